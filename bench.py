@@ -1,0 +1,247 @@
+"""bench.py -- BASELINE.json metric: env steps/s at N=65536 parallel envs on
+pointmaze-large (pointmaze-large-navigate-v0), 1/2/4/8 MI355X.
+
+    python bench.py --gpus N --steps K --warmup W [--workload pointmaze|powder|gcsample]
+
+A step = one ``env.step(action)`` of all envs of this rank: one launch of
+``maze_step_kernel`` through the C-ABI (Python -> ctypes -> libogbx), with the
+[N,2] float32 actions already resident in HBM (pre-generated ring, seed 1) and
+same-step auto-reset.  Timed region: barrier + synchronize, K steps, barrier +
+synchronize; the max over ranks is reported.  Multi-GPU: one process per GPU,
+each rank owns its own 65536 envs (independent shards, no data-path
+collective) -> "scaling": "weak"; ``value`` = envs x steps of all ranks / time.
+
+Extra fields (not ``value``): the same workload replayed from a hipGraph and
+as K fused steps per launch; ``roofline`` of maze_step_kernel (algorithmic
+87 B per env-step) from per-launch HIP events on the launch stream;
+``cpu_baseline`` = the oracle C restatement (OpenMP) on a bounded sample.
+"""
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def _dist_init():
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(local)
+    return world, rank, local
+
+
+def _barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def _max_over_ranks(x, world, dev):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _timed(fn, steps, world, dev):
+    _barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        fn(i)
+    torch.cuda.synchronize(dev)
+    _barrier(world)
+    dt = time.perf_counter() - t0
+    return _max_over_ranks(dt, world, dev)
+
+
+def _per_launch_ms(fn, launches, dev):
+    """Average device duration of single launches: HIP event pair around each
+    launch, on the stream the kernel runs on (torch's current stream)."""
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    for i, (a, b) in enumerate(ev):
+        a.record(stream)
+        fn(i)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def bench_pointmaze(args, world, rank, dev):
+    import ogbench_amd
+
+    n = args.num_envs
+    env = ogbench_amd.make('pointmaze-large-v0', num_envs=n, device=dev, auto_reset=True)
+    task = (torch.arange(n, dtype=torch.int32, device=dev) % 5) + 1
+    env.reset(seed=rank, options=dict(task_id=task))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + 1000 * rank)
+    ring = args.ring
+    actions = torch.rand(ring, n, 2, device=dev, generator=gen, dtype=torch.float32) * 2 - 1
+
+    def step(i):
+        env.step(actions[i % ring])
+
+    for i in range(args.warmup):
+        step(i)
+    dt = _timed(step, args.steps, world, dev)
+    total_env_steps = n * args.steps * world
+    value = total_env_steps / dt
+    ms_per_step = dt / args.steps * 1e3
+
+    # kernel duration for the roofline (same workload, untimed pass)
+    kern_ms = _per_launch_ms(step, min(args.steps, 200), dev)
+    alg_bytes = 87 * n  # 87 B per env-step
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+
+    extra = {}
+    # hipGraph replay of G steps (launch-bound inner loop captured once)
+    try:
+        G = 32
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for i in range(3):
+                step(i)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for i in range(G):
+                step(i)
+        for _ in range(3):
+            graph.replay()
+        reps = max(1, args.steps // G)
+        gdt = _timed(lambda i: graph.replay(), reps, world, dev)
+        extra['graph_replay_steps_per_s'] = n * G * reps * world / gdt
+    except Exception as e:  # pragma: no cover - reported, not fatal
+        extra['graph_replay_error'] = repr(e)[:200]
+    # K fused steps per launch
+    K = 64
+    fused_actions = actions[:K].contiguous()
+    out = None
+
+    def fused(i):
+        nonlocal out
+        out = env.rollout(fused_actions, out)
+
+    fused(0)
+    reps = max(1, args.steps // K)
+    fdt = _timed(fused, reps, world, dev)
+    extra['fused_k64_steps_per_s'] = n * K * reps * world / fdt
+    fk_ms = _per_launch_ms(fused, 5, dev)
+    fused_bytes = (8 + 16 + 4 + 3) * n * K + (16 + 16 + 4 + 4 + 16 + 4 + 4) * n
+    extra['fused_k64_kernel_ms'] = fk_ms
+    extra['fused_k64_achieved_GBs'] = fused_bytes / (fk_ms * 1e-3) / 1e9
+
+    result = dict(
+        metric='env steps/sec at N=65536 parallel envs, pointmaze-large, 1/2/4/8 MI355X',
+        value=value,
+        unit='env_steps/s',
+        n_gpus=world,
+        steps=args.steps,
+        warmup=args.warmup,
+        ms_per_step=ms_per_step,
+        higher_is_better=True,
+        scaling='weak',
+        vs_baseline=None,
+        dtype='f64',
+        data='synthetic (uniform [-1,1] float32 actions, Philox reset noise; no dataset)',
+        config=dict(
+            workload='pointmaze-large-navigate-v0',
+            num_envs_per_gpu=n,
+            total_envs=n * world,
+            auto_reset=True,
+            task_id='i%5+1',
+            parallelism=f'env-shard x{world}',
+        ),
+        roofline=dict(
+            bound='hbm',
+            kernel='maze_step_kernel',
+            achieved=achieved,
+            peak=HBM_PEAK_GBS,
+            unit='GB/s',
+            frac=achieved / HBM_PEAK_GBS,
+            traffic=None,
+            kernel_ms=kern_ms,
+            alg_bytes_per_launch=alg_bytes,
+        ),
+        extra=extra,
+    )
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline_pointmaze(n, args)
+    env.close()
+    return result
+
+
+def cpu_baseline_pointmaze(n, args):
+    """The oracle C restatement (kind 'port'), OpenMP over envs, bounded sample."""
+    from oracle import locomaze as orc
+
+    threads = int(os.environ.get('OMP_NUM_THREADS', '16'))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    rng = np.random.RandomState(0)
+    tid = (np.arange(n) % 5 + 1).astype(np.int32)
+    st = orc.reset('large', tid, rng.uniform(-1, 1, (n, 4)))
+    steps, t0 = 0, time.perf_counter()
+    budget = args.cpu_seconds
+    while time.perf_counter() - t0 < budget:
+        a = rng.uniform(-1, 1, (1, n, 2)).astype(np.float32)
+        orc.step('large', st, a, auto_reset=1, key=(0, 0), nthreads=threads)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return dict(
+        value=n * steps / dt,
+        unit='env_steps/s',
+        cores=threads,
+        kind='port',
+        sample=f'{steps} steps x {n} envs of pointmaze-large with auto-reset ({dt:.1f} s)',
+    )
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=2000)
+    ap.add_argument('--warmup', type=int, default=100)
+    ap.add_argument('--workload', default='pointmaze', choices=['pointmaze'])
+    ap.add_argument('--num-envs', type=int, default=65536)
+    ap.add_argument('--ring', type=int, default=128)
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+    world, rank, local = _dist_init()
+    if world != args.gpus and rank == 0:
+        print(f'# note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE', flush=True)
+    dev = torch.device('cuda', local)
+    import sys
+
+    sys.path.insert(0, ROOT)
+    result = bench_pointmaze(args, world, rank, dev)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

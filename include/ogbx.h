@@ -1,0 +1,165 @@
+/*
+ * ogbx.h -- C-ABI of the MI355X-native OGBench hot path (libogbx.so, gfx950).
+ *
+ * This header is the drop-in boundary. Every entry point replaces one reference
+ * interface; the reference file:line it stands in for is cited next to it
+ * (paths relative to hliuson/ogbench).  Types are plain C: device pointers,
+ * sizes, an opaque handle and a hipStream_t passed as `void*`.  No torch types
+ * cross this boundary; the Python layer (ogbench_amd/) passes
+ * `tensor.data_ptr()` and `torch.cuda.current_stream().cuda_stream`.
+ *
+ * Conventions (all entry points):
+ *   - Every call returns an ogbx_status; on failure ogbx_last_error() holds a
+ *     thread-local message.  Status codes never become exceptions here; the
+ *     Python layer raises ValueError/AssertionError/RuntimeError exactly where
+ *     the reference does (maze.py:29,163,347,379,384).
+ *   - All I/O buffers are caller-owned DEVICE memory.  A handle owns only its
+ *     static tables (maze map, task table, goal worlds), its per-env state and
+ *     its RNG counters.
+ *   - Calls are asynchronous on `stream`; nothing synchronises the host except
+ *     the explicit *_sync / *_read_state helpers.
+ *   - One handle per (device, stream) at a time; distinct handles are
+ *     independent, so one process may drive several GPUs.
+ *   - There is no CPU fallback: a handle can only be created on a visible
+ *     gfx950 device, otherwise OGBX_EDEVICE.
+ */
+#ifndef OGBX_H
+#define OGBX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OGBX_ABI_VERSION 1
+
+typedef enum {
+  OGBX_OK = 0,
+  OGBX_EINVAL = -1,  /* bad argument (reference: ValueError / AssertionError) */
+  OGBX_EDEVICE = -2, /* HIP runtime error or no gfx950 device */
+  OGBX_ENOMEM = -3,  /* device allocation failed */
+  OGBX_ESTATE = -4   /* handle used in the wrong state (e.g. step before reset) */
+} ogbx_status;
+
+/* Thread-local message describing the last failure of this thread. */
+const char* ogbx_last_error(void);
+/* OGBX_ABI_VERSION of the loaded library. */
+int32_t ogbx_abi_version(void);
+/* Name of the GPU architecture the library was built for ("gfx950"). */
+const char* ogbx_build_arch(void);
+
+/* ======================================================================
+ * Locomaze (pointmaze) batched environment
+ * ====================================================================== */
+
+typedef struct ogbx_maze_env* ogbx_maze_t;
+
+/* Static options of a batch of MazeEnv instances.
+ * Reference: MazeEnv.__init__ kwargs, ogbench/locomaze/maze.py:37-86, and the
+ * registry kwargs in ogbench/locomaze/__init__.py:10-13,16-35,248-275. */
+typedef struct {
+  int32_t loco_type;         /* 0 = point (PointEnv dynamics, point.py:64-95).
+                                1 = ant, 2 = humanoid: wrapper only (goal/time/
+                                reward logic, maze.py:433-466); dynamics are out
+                                of scope and such handles reject step(). */
+  int32_t success_timing;    /* 0 = 'post' (default, maze.py:43), 1 = 'pre'. */
+  int32_t terminate_at_goal; /* maze.py:42, default 1. */
+  int32_t add_noise_to_goal; /* maze.py:45, default 1 (0 for singletask). */
+  int32_t reward_task_id;    /* -1 = goal-conditioned (None); 0 => default task 1
+                                (maze.py:361-362); 1..num_tasks single-task. */
+  int32_t max_episode_steps; /* TimeLimit, locomaze/__init__.py:20 (1000). */
+} ogbx_maze_opts;
+
+/* Create a batch of `n_envs` maze envs on `device`.
+ * maze_type: "arena" | "medium" | "large" | "giant" | "teleport"
+ * (maze.py:90-163; anything else -> OGBX_EINVAL, reference ValueError at :163).
+ * Replaces: make_maze_env(...) + gymnasium.make (maze.py:13-218). */
+ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t device,
+                             const ogbx_maze_opts* opts, ogbx_maze_t* out);
+ogbx_status ogbx_maze_destroy(ogbx_maze_t env);
+/* Number of envs of the handle. */
+int64_t ogbx_maze_num_envs(ogbx_maze_t env);
+
+/* Static description: H, W of the map, number of tasks, goal_tol
+ * (maze.py:86: 1.0 point / 0.5 ant+humanoid), maze_unit (4.0). */
+ogbx_status ogbx_maze_describe(ogbx_maze_t env, int32_t* map_h, int32_t* map_w,
+                               int32_t* num_tasks, double* goal_tol, double* maze_unit);
+/* Copy the map (row-major int32 [H*W], 1 = wall) and the task table
+ * (int32 [num_tasks*4] = init_i, init_j, goal_i, goal_j; maze.py:308-359)
+ * to HOST buffers. Either pointer may be NULL. */
+ogbx_status ogbx_maze_tables(ogbx_maze_t env, int32_t* map_out, int32_t* tasks_out);
+
+/* Device-free query of the static maze tables (used by host-side checks):
+ * map_h/map_w/num_tasks out; map_out int32[H*W] and tasks_out int32[num_tasks*4]
+ * may be NULL (query sizes first).  Unknown maze_type -> OGBX_EINVAL. */
+ogbx_status ogbx_maze_static_tables(const char* maze_type, int32_t* map_h, int32_t* map_w,
+                                    int32_t* num_tasks, int32_t* map_out, int32_t* tasks_out);
+
+/* Reset the envs selected by `mask` (device u8[N]; NULL = all).
+ * Reference: MazeEnv.reset, maze.py:373-431 (+ PointEnv.set_xy point.py:111-115).
+ *   task_id  device i32[N], values in 1..num_tasks; NULL = keep/draw: a single-
+ *            task handle always uses reward_task_id; otherwise NULL draws a
+ *            uniform task from the Philox stream (maze.py:391-394).
+ *            Values are validated by the caller (the Python layer raises the
+ *            reference AssertionError); out-of-range values fall back to 1.
+ *   task_xy  device f64[N,4] (init_x, init_y, goal_x, goal_y) or NULL; when given
+ *            it replaces the task table, i.e. options['task_info'] (maze.py:387-
+ *            390) with the cell centres already converted by ij_to_xy.
+ *   noise    device f64[N,4] = the four np.random.uniform(-1,1) draws in reset
+ *            order (init x, init y, goal x, goal y; maze.py:402-405,564-567) or
+ *            NULL = draw them from Philox4x32-10 keyed by (seed, env index,
+ *            episode counter).
+ *   obs      device f64[N,2] out (ob = init_xy), goal device f64[N,2] out
+ *            (info['goal'] = goal_xy, maze.py:416-427).  Rows of masked-out envs
+ *            are left untouched. */
+ogbx_status ogbx_maze_reset(ogbx_maze_t env, const int32_t* task_id, const double* task_xy,
+                            const uint8_t* mask, const double* noise, double* obs, double* goal,
+                            uint64_t seed, void* stream);
+
+/* Step all N envs `k_steps` times with actions device [k_steps, N, 2]
+ * (float32 if action_is_f64 == 0, float64 otherwise) in ONE launch.
+ * Reference per step: TimeLimit -> MazeEnv.step (maze.py:433-466) ->
+ * PointEnv.step (point.py:64-95) -> mujoco.mj_step(nstep=5) (point.py:73).
+ * Outputs are [k_steps, N] rows (obs [k_steps, N, 2]):
+ *   obs f64, reward f32 (1/0, or -1/0 single-task), terminated/truncated/
+ *   success u8.  final_obs (nullable) receives the pre-reset observation of envs
+ *   that auto-reset at that step (gymnasium same-step autoreset).
+ * auto_reset != 0: envs that end (terminated|truncated) are reset in the same
+ *   step with Philox noise (seed given at the last ogbx_maze_reset) keeping
+ *   their task; obs then holds the new initial observation. */
+ogbx_status ogbx_maze_step(ogbx_maze_t env, const void* action, int32_t action_is_f64,
+                           int32_t k_steps, double* obs, float* reward, uint8_t* terminated,
+                           uint8_t* truncated, uint8_t* success, double* final_obs,
+                           int32_t auto_reset, void* stream);
+
+/* Device pointers of the env-owned state (for checkpoint/restore and tests):
+ * qpos f64[N,2], goal_xy f64[N,2], elapsed i32[N], task_id i32[N]. */
+ogbx_status ogbx_maze_state(ogbx_maze_t env, double** qpos, double** goal_xy, int32_t** elapsed,
+                            int32_t** task_id);
+
+/* Free-standing physics: advance `n` point masses one PointEnv step without
+ * any env bookkeeping: qpos_out = mj_step^5(qpos + 0.2*action).  Used by the
+ * parity tests for arbitrary (qpos, action) pairs.  Replaces point.py:68-73. */
+ogbx_status ogbx_point_physics(ogbx_maze_t env, const double* qpos_in, const void* action,
+                               int32_t action_is_f64, int64_t n, double* qpos_out,
+                               uint8_t* contact_out, void* stream);
+
+/* Batched coordinate helpers (maze.py:552-562): xy f64[n,2] -> ij i32[n,2]
+ * with Python int() truncation toward zero, and ij -> xy. */
+ogbx_status ogbx_maze_xy_to_ij(ogbx_maze_t env, const double* xy, int64_t n, int32_t* ij,
+                               void* stream);
+ogbx_status ogbx_maze_ij_to_xy(ogbx_maze_t env, const int32_t* ij, int64_t n, double* xy,
+                               void* stream);
+
+/* Oracle subgoal (maze.py:503-550) for n (start_xy, goal_xy) pairs:
+ * BFS next-hop from a device table built at create time.  subgoal f64[n,2]. */
+ogbx_status ogbx_maze_oracle_subgoal(ogbx_maze_t env, const double* start_xy,
+                                     const double* goal_xy, int64_t n, double* subgoal_xy,
+                                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OGBX_H */

@@ -1,0 +1,732 @@
+// locomaze.hip -- batched pointmaze envs on gfx950: reset / step / physics kernels
+// and their C-ABI (include/ogbx.h).
+//
+// Layout in HBM (one handle = one batch of N envs on one device):
+//   qpos    f64[N,2]  (x, y interleaved: one 16-B load/store per lane)
+//   goal    f64[N,2]
+//   elapsed i32[N]    TimeLimit counter (gymnasium TimeLimit, max_episode_steps)
+//   task    i32[N]    1-based task id of the running episode
+//   episode u32[N]    per-env reset counter (Philox counter word)
+// Static tables (map, tasks, teleports, model constants) travel as one by-value
+// kernel argument; the map is staged into LDS at block start.
+//
+// Reference behaviour restated here (paths relative to hliuson/ogbench):
+//   MazeEnv.reset   ogbench/locomaze/maze.py:373-431
+//   MazeEnv.step    ogbench/locomaze/maze.py:433-466
+//   compute_success ogbench/locomaze/maze.py:486-490
+//   xy_to_ij / ij_to_xy / add_noise  maze.py:552-567
+//   PointEnv.step   ogbench/locomaze/point.py:64-95
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "point_physics.h"
+
+namespace ogbx {
+
+constexpr int kMaxCells = 256;
+constexpr int kMaxTasks = 8;
+
+struct MazeParams {
+  PointModel pm;
+  int32_t H, W, num_tasks, loco_type;
+  int32_t success_pre, terminate_at_goal, add_noise_to_goal, reward_task_id;
+  int32_t max_steps, n_tp_in, n_tp_out, pad_;
+  double goal_tol, tp_radius;
+  double tp_in[2][2];
+  double tp_out[3][2];
+  int32_t tasks[kMaxTasks][4];  // init_i, init_j, goal_i, goal_j
+  uint8_t wall[kMaxCells];
+};
+
+struct MazeState {
+  double* qpos;
+  double* goal;
+  int32_t* elapsed;
+  int32_t* task;
+  uint32_t* episode;
+};
+
+}  // namespace ogbx
+
+struct ogbx_maze_env {
+  int32_t device = 0;
+  int64_t n = 0;
+  ogbx::MazeParams P;
+  ogbx::MazeState S{};
+  ogbx::MazeParams* Pd = nullptr;  // device copy of P (tables indexed per lane)
+  int16_t* bfs = nullptr;  // [H*W goal cell][H*W cell] BFS distances (maze.py:517-536)
+  uint64_t seed = 0;
+  bool was_reset = false;
+};
+
+namespace ogbx {
+
+// ------------------------------------------------------------ device helpers
+
+__device__ inline void stage_wall(const MazeParams& P, uint8_t* wall_s) {
+  for (int t = threadIdx.x; t < P.H * P.W; t += blockDim.x) wall_s[t] = P.wall[t];
+  __syncthreads();
+}
+
+// np.linalg.norm(xy - goal) <= tol with the 1-D OpenBLAS ddot rounding:
+// sqrt(fma(dy, dy, dx*dx)) (maze.py:487).
+__device__ inline bool goal_reached(double x, double y, double gx, double gy, double tol) {
+  double dx = x - gx, dy = y - gy;
+  return sqrt(fma(dy, dy, dx * dx)) <= tol;
+}
+
+// The four uniform(-1, 1) reset draws of one env, in reference order
+// (init x, init y, goal x, goal y).
+__device__ inline void reset_draws(uint64_t i, uint32_t ep, uint32_t k0, uint32_t k1,
+                                   double r[4]) {
+  u32x4 a = philox4x32_10({(uint32_t)i, ep, 0u, (uint32_t)(i >> 32)}, k0, k1);
+  u32x4 b = philox4x32_10({(uint32_t)i, ep, 1u, (uint32_t)(i >> 32)}, k0, k1);
+  r[0] = -1.0 + 2.0 * u01_from(a.x, a.y);
+  r[1] = -1.0 + 2.0 * u01_from(a.z, a.w);
+  r[2] = -1.0 + 2.0 * u01_from(b.x, b.y);
+  r[3] = -1.0 + 2.0 * u01_from(b.z, b.w);
+}
+
+__device__ inline int32_t draw_task(const MazeParams& P, uint64_t i, uint32_t ep, uint32_t k0,
+                                    uint32_t k1) {
+  u32x4 c = philox4x32_10({(uint32_t)i, ep, 2u, (uint32_t)(i >> 32)}, k0, k1);
+  return 1 + (int32_t)bounded_u32(c.x, (uint32_t)P.num_tasks);
+}
+
+// MazeEnv.reset for one env: returns init (x, y) and goal (gx, gy).
+// add_noise: xy + uniform(-1,1) * maze_unit / 4 (maze.py:564-567).
+__device__ inline void reset_one(const MazeParams& P, int32_t task, const double* task_xy,
+                                 const double r[4], double& x, double& y, double& gx,
+                                 double& gy) {
+  double ix, iy, bx, by;
+  if (task_xy != nullptr) {
+    ix = task_xy[0];
+    iy = task_xy[1];
+    bx = task_xy[2];
+    by = task_xy[3];
+  } else {
+    const int32_t* t = P.tasks[task - 1];
+    ix = t[1] * P.pm.unit - P.pm.off_x;
+    iy = t[0] * P.pm.unit - P.pm.off_y;
+    bx = t[3] * P.pm.unit - P.pm.off_x;
+    by = t[2] * P.pm.unit - P.pm.off_y;
+  }
+  x = ix + r[0] * P.pm.unit / 4.0;
+  y = iy + r[1] * P.pm.unit / 4.0;
+  if (P.add_noise_to_goal) {
+    gx = bx + r[2] * P.pm.unit / 4.0;
+    gy = by + r[3] * P.pm.unit / 4.0;
+  } else {
+    gx = bx;
+    gy = by;
+  }
+}
+
+// ------------------------------------------------------------------ kernels
+
+__global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __restrict__ Pp, MazeState S, int64_t n,
+                                                         const int32_t* task_id,
+                                                         const double* task_xy,
+                                                         const uint8_t* mask, const double* noise,
+                                                         double* obs, double* goal_out,
+                                                         uint32_t k0, uint32_t k1) {
+  const MazeParams& P = *Pp;
+  const PointModel pm = P.pm;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (mask != nullptr && mask[i] == 0) return;
+  uint32_t ep = S.episode[i] + 1u;
+  int32_t task;
+  if (P.reward_task_id > 0) task = P.reward_task_id;
+  else if (task_id != nullptr) task = task_id[i];
+  else task = draw_task(P, (uint64_t)i, ep, k0, k1);
+  if (task < 1 || task > P.num_tasks) task = 1;  // validated on the host
+  double r[4];
+  if (noise != nullptr) {
+    r[0] = noise[4 * i + 0];
+    r[1] = noise[4 * i + 1];
+    r[2] = noise[4 * i + 2];
+    r[3] = noise[4 * i + 3];
+  } else {
+    reset_draws((uint64_t)i, ep, k0, k1, r);
+  }
+  double x, y, gx, gy;
+  reset_one(P, task, task_xy ? task_xy + 4 * i : nullptr, r, x, y, gx, gy);
+  S.qpos[2 * i] = x;
+  S.qpos[2 * i + 1] = y;
+  S.goal[2 * i] = gx;
+  S.goal[2 * i + 1] = gy;
+  S.elapsed[i] = 0;
+  S.task[i] = task;
+  S.episode[i] = ep;
+  obs[2 * i] = x;
+  obs[2 * i + 1] = y;
+  goal_out[2 * i] = gx;
+  goal_out[2 * i + 1] = gy;
+}
+
+// One launch = k_steps consecutive env steps of every env; state stays in
+// registers across the k loop.  One lane per env.
+template <bool kF64>
+__global__ void __launch_bounds__(256) maze_step_kernel(
+    const MazeParams* __restrict__ Pp, MazeState S, int64_t n, const void* __restrict__ action_v,
+    int32_t k_steps,
+    double* __restrict__ obs, float* __restrict__ reward, uint8_t* __restrict__ terminated,
+    uint8_t* __restrict__ truncated, uint8_t* __restrict__ success,
+    double* __restrict__ final_obs, int32_t auto_reset, uint32_t k0, uint32_t k1) {
+  const MazeParams& P = *Pp;
+  const PointModel pm = P.pm;
+  __shared__ uint8_t wall_s[kMaxCells];
+  stage_wall(P, wall_s);
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+
+  double2 q = reinterpret_cast<const double2*>(S.qpos)[i];
+  double2 g = reinterpret_cast<const double2*>(S.goal)[i];
+  int32_t el = S.elapsed[i];
+  int32_t task = S.task[i];
+  uint32_t ep = S.episode[i];
+  double x = q.x, y = q.y, gx = g.x, gy = g.y;
+
+  for (int32_t k = 0; k < k_steps; ++k) {
+    const int64_t o = (int64_t)k * n + i;
+    double dx, dy;
+    if (kF64) {
+      double2 a = reinterpret_cast<const double2*>(action_v)[o];
+      dx = 0.2 * a.x;
+      dy = 0.2 * a.y;
+    } else {
+      float2 a = reinterpret_cast<const float2*>(action_v)[o];
+      dx = (double)(0.2f * a.x);  // float32 * weak python float stays float32 (NEP 50)
+      dy = (double)(0.2f * a.y);
+    }
+    bool succ = false;
+    if (P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
+    x = x + dx;
+    y = y + dy;
+    point_step(pm, wall_s, P.H, P.W, &x, &y);
+    if (!P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
+    const double ox = x, oy = y;  // ob is taken before a teleport (maze.py:437-451)
+    if (P.n_tp_in > 0) {
+      for (int t = 0; t < P.n_tp_in; ++t) {
+        if (goal_reached(x, y, P.tp_in[t][0], P.tp_in[t][1], P.tp_radius * 1.5)) {
+          u32x4 c = philox4x32_10({(uint32_t)i, ep, 0x100u + (uint32_t)el, (uint32_t)(i >> 32)},
+                                  k0 ^ kTagMazeTeleport, k1);
+          int o_idx = (int)bounded_u32(c.x, (uint32_t)P.n_tp_out);
+          x = P.tp_out[o_idx][0];
+          y = P.tp_out[o_idx][1];
+          break;
+        }
+      }
+    }
+    float rew = succ ? 1.0f : 0.0f;
+    if (P.reward_task_id > 0) rew -= 1.0f;
+    const bool term = succ && P.terminate_at_goal;
+    el += 1;
+    const bool trunc = el >= P.max_steps;
+    reward[o] = rew;
+    terminated[o] = term;
+    truncated[o] = trunc;
+    success[o] = succ;
+    double wx = ox, wy = oy;
+    if (auto_reset && (term || trunc)) {
+      if (final_obs != nullptr) reinterpret_cast<double2*>(final_obs)[o] = make_double2(ox, oy);
+      ep += 1u;
+      double r[4];
+      reset_draws((uint64_t)i, ep, k0, k1, r);
+      reset_one(P, task, nullptr, r, x, y, gx, gy);
+      el = 0;
+      wx = x;
+      wy = y;
+    }
+    reinterpret_cast<double2*>(obs)[o] = make_double2(wx, wy);
+  }
+  reinterpret_cast<double2*>(S.qpos)[i] = make_double2(x, y);
+  reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
+  S.elapsed[i] = el;
+  S.episode[i] = ep;
+}
+
+template <bool kF64>
+__global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __restrict__ Pp,
+                                                            const double* qpos_in,
+                                                            const void* action_v, int64_t n,
+                                                            double* qpos_out,
+                                                            uint8_t* contact_out) {
+  const MazeParams& P = *Pp;
+  const PointModel pm = P.pm;
+  __shared__ uint8_t wall_s[kMaxCells];
+  stage_wall(P, wall_s);
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x = qpos_in[2 * i], y = qpos_in[2 * i + 1];
+  if (kF64) {
+    const double* a = (const double*)action_v;
+    x = x + 0.2 * a[2 * i];
+    y = y + 0.2 * a[2 * i + 1];
+  } else {
+    const float* a = (const float*)action_v;
+    x = x + (double)(0.2f * a[2 * i]);
+    y = y + (double)(0.2f * a[2 * i + 1]);
+  }
+  int c = point_step(pm, wall_s, P.H, P.W, &x, &y);
+  qpos_out[2 * i] = x;
+  qpos_out[2 * i + 1] = y;
+  if (contact_out) contact_out[i] = (uint8_t)c;
+}
+
+// xy_to_ij: i = int((y + off_y + 0.5*unit)/unit) with Python int() truncation
+// toward zero (maze.py:552-556).
+__global__ void xy_to_ij_kernel(const MazeParams* __restrict__ Pp, const double* xy, int64_t n, int32_t* ij) {
+  const MazeParams& P = *Pp;
+  const PointModel pm = P.pm;
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  double x = xy[2 * t], y = xy[2 * t + 1];
+  double fi = (y + P.pm.off_y + 0.5 * P.pm.unit) / P.pm.unit;
+  double fj = (x + P.pm.off_x + 0.5 * P.pm.unit) / P.pm.unit;
+  fi = fmin(fmax(fi, -2147483648.0), 2147483647.0);
+  fj = fmin(fmax(fj, -2147483648.0), 2147483647.0);
+  ij[2 * t] = (int32_t)fi;
+  ij[2 * t + 1] = (int32_t)fj;
+}
+
+__global__ void ij_to_xy_kernel(const MazeParams* __restrict__ Pp, const int32_t* ij, int64_t n, double* xy) {
+  const MazeParams& P = *Pp;
+  const PointModel pm = P.pm;
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  xy[2 * t] = ij[2 * t + 1] * P.pm.unit - P.pm.off_x;
+  xy[2 * t + 1] = ij[2 * t] * P.pm.unit - P.pm.off_y;
+}
+
+__device__ inline int clamp_idx(double f, int hi) {
+  f = fmin(fmax(f, -1.0), (double)hi);
+  int v = (int)f;
+  return v < 0 ? 0 : (v > hi - 1 ? hi - 1 : v);
+}
+
+// get_oracle_subgoal (maze.py:503-550) from the precomputed BFS table.
+__global__ void oracle_subgoal_kernel(const MazeParams* __restrict__ Pp, const int16_t* bfs, const double* start_xy,
+                                      const double* goal_xy, int64_t n, double* sub_xy) {
+  const MazeParams& P = *Pp;
+  const PointModel pm = P.pm;
+  __shared__ uint8_t wall_s[kMaxCells];
+  stage_wall(P, wall_s);
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int H = P.H, W = P.W;
+  int si = clamp_idx((start_xy[2 * t + 1] + P.pm.off_y + 0.5 * P.pm.unit) / P.pm.unit, H);
+  int sj = clamp_idx((start_xy[2 * t] + P.pm.off_x + 0.5 * P.pm.unit) / P.pm.unit, W);
+  int gi = clamp_idx((goal_xy[2 * t + 1] + P.pm.off_y + 0.5 * P.pm.unit) / P.pm.unit, H);
+  int gj = clamp_idx((goal_xy[2 * t] + P.pm.off_x + 0.5 * P.pm.unit) / P.pm.unit, W);
+  const int16_t* d = bfs + (int64_t)(gi * W + gj) * (H * W);
+  int bi = si, bj = sj;
+  const int di[4] = {-1, 0, 1, 0}, dj[4] = {0, -1, 0, 1};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int ni = si + di[k], nj = sj + dj[k];
+    if (ni >= 0 && ni < H && nj >= 0 && nj < W && wall_s[ni * W + nj] == 0 &&
+        d[ni * W + nj] < d[bi * W + bj]) {
+      bi = ni;
+      bj = nj;
+    }
+  }
+  sub_xy[2 * t] = bj * P.pm.unit - P.pm.off_x;
+  sub_xy[2 * t + 1] = bi * P.pm.unit - P.pm.off_y;
+}
+
+// ------------------------------------------------------------- host tables
+
+struct MazeSpec {
+  const char* name;
+  int H, W;
+  const char* rows;  // H*W chars '1'/'0'
+  int ntasks;
+  int tasks[5][4];
+};
+
+// Maps: maze.py:90-150.  Tasks: maze.py:310-345.
+static const MazeSpec kMazes[] = {
+    {"arena", 8, 8,
+     "11111111"
+     "10000001"
+     "10000001"
+     "10000001"
+     "10000001"
+     "10000001"
+     "10000001"
+     "11111111",
+     1, {{1, 1, 6, 6}}},
+    {"medium", 8, 8,
+     "11111111"
+     "10011001"
+     "10010001"
+     "11000111"
+     "10010001"
+     "10100101"
+     "10001001"
+     "11111111",
+     5, {{1, 1, 6, 6}, {6, 1, 1, 6}, {5, 3, 4, 2}, {6, 5, 6, 1}, {2, 6, 1, 1}}},
+    {"large", 9, 12,
+     "111111111111"
+     "100001000001"
+     "101101010101"
+     "100000010001"
+     "101111011101"
+     "100101000001"
+     "110101010111"
+     "100100010001"
+     "111111111111",
+     5, {{1, 1, 7, 10}, {5, 4, 7, 1}, {7, 4, 1, 10}, {3, 8, 5, 4}, {1, 1, 5, 4}}},
+    {"giant", 12, 16,
+     "1111111111111111"
+     "1010000001100001"
+     "1010110101001101"
+     "1000100100010001"
+     "1011101111110101"
+     "1000100010000101"
+     "1110101001010111"
+     "1000100100010001"
+     "1010101111110101"
+     "1011100010001101"
+     "1000001000100001"
+     "1111111111111111",
+     5, {{1, 1, 10, 14}, {1, 14, 10, 1}, {8, 14, 1, 1}, {8, 3, 5, 12}, {5, 9, 3, 8}}},
+    {"teleport", 9, 12,
+     "111111111111"
+     "100000101001"
+     "110100010011"
+     "110111000001"
+     "100001010101"
+     "101101010101"
+     "101101010101"
+     "100001000101"
+     "111111111111",
+     5, {{1, 10, 7, 1}, {1, 1, 7, 10}, {5, 6, 7, 10}, {7, 1, 7, 10}, {5, 6, 7, 1}}},
+};
+
+// MuJoCo-derived constants of the point model (DESIGN.md lists each source).
+static PointModel make_point_model(double unit, double off) {
+  PointModel pm{};
+  const double pi = 3.14159265358979323846;
+  const double r = 0.7, density = 100.0;
+  pm.mass = density * (4.0 * pi * r * r * r / 3.0);
+  pm.h = 0.02;
+  pm.nsub = 5;
+  // solref (0.02, 1) with refsafe: timeconst = max(0.02, 2*dt) = 0.04
+  const double timeconst = std::fmax(0.02, 2.0 * pm.h), dampratio = 1.0;
+  // solimp (0.9, 0.95, 0.001, 0.5, 2)
+  pm.imp_dmin = 0.9;
+  pm.imp_dmax = 0.95;
+  pm.imp_width = 0.001;
+  pm.imp_mid = 0.5;
+  pm.imp_power = 2.0;
+  const double dmax = pm.imp_dmax;
+  pm.K = 1.0 / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
+  pm.B = 2.0 / (dmax * timeconst);
+  // body_invweight0 (translation) = mean diag of J M^-1 J' over 3 axes = 2/(3m);
+  // pyramid edge diagApprox = tran + mu^2 * tran with mu = 1.
+  const double tran = (1.0 / pm.mass + 1.0 / pm.mass + 0.0) / 3.0;
+  const double mu = 1.0;
+  pm.diag = tran + mu * mu * tran;
+  double Rf = (1.0 - pm.imp_dmin) * pm.diag / pm.imp_dmin;
+  if (Rf < kMinVal) Rf = kMinVal;
+  // Floor: four edges +-e_x, +-e_y, each with D = 1/Rf; exactly one edge of
+  // each pair is active, which sums to 1/2 Df |a + B v|^2.
+  pm.D_floor = 1.0 / Rf;
+  pm.radius = r;
+  pm.sphere_z = 0.7;
+  pm.box_cz = 0.5 / 2.0 * unit;  // maze_height/2 * maze_unit (maze.py:233)
+  pm.box_hz = 0.5 / 2.0 * unit;
+  pm.box_hxy = unit / 2.0;
+  pm.unit = unit;
+  pm.off_x = off;
+  pm.off_y = off;
+  return pm;
+}
+
+static void build_bfs(const MazeParams& P, std::vector<int16_t>& out) {
+  const int H = P.H, W = P.W, C = H * W;
+  out.assign((size_t)C * C, -1);
+  for (int g = 0; g < C; ++g) {
+    int16_t* d = out.data() + (size_t)g * C;
+    std::deque<int> qu;
+    d[g] = 0;
+    qu.push_back(g);
+    const int di[4] = {-1, 0, 1, 0}, dj[4] = {0, -1, 0, 1};
+    while (!qu.empty()) {
+      int c = qu.front();
+      qu.pop_front();
+      int i = c / W, j = c % W;
+      for (int k = 0; k < 4; ++k) {
+        int ni = i + di[k], nj = j + dj[k];
+        if (ni >= 0 && ni < H && nj >= 0 && nj < W && P.wall[ni * W + nj] == 0 &&
+            d[ni * W + nj] == -1) {
+          d[ni * W + nj] = (int16_t)(d[c] + 1);
+          qu.push_back(ni * W + nj);
+        }
+      }
+    }
+  }
+}
+
+static inline uint32_t grid_for(int64_t n, int block) { return (uint32_t)((n + block - 1) / block); }
+
+}  // namespace ogbx
+
+using namespace ogbx;
+
+extern "C" {
+
+ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t device,
+                             const ogbx_maze_opts* opts, ogbx_maze_t* out) {
+  OGBX_CHECK(out != nullptr && maze_type != nullptr && opts != nullptr, OGBX_EINVAL,
+             "ogbx_maze_create: null argument");
+  *out = nullptr;
+  OGBX_CHECK(n_envs > 0 && n_envs <= (int64_t)1 << 32, OGBX_EINVAL,
+             "ogbx_maze_create: n_envs must be in [1, 2^32]");
+  const MazeSpec* spec = nullptr;
+  for (const auto& s : kMazes)
+    if (std::strcmp(s.name, maze_type) == 0) spec = &s;
+  OGBX_CHECK(spec != nullptr, OGBX_EINVAL, std::string("Unknown maze type: ") + maze_type);
+  OGBX_CHECK(opts->loco_type >= 0 && opts->loco_type <= 2, OGBX_EINVAL,
+             "Unknown locomotion environment type");
+  OGBX_CHECK(opts->success_timing == 0 || opts->success_timing == 1, OGBX_EINVAL,
+             "success_timing must be 'pre' or 'post'");
+  OGBX_CHECK(opts->max_episode_steps > 0, OGBX_EINVAL, "max_episode_steps must be positive");
+  OGBX_CHECK(opts->reward_task_id <= spec->ntasks, OGBX_EINVAL,
+             "Task ID must be in [1, " + std::to_string(spec->ntasks) + "].");
+  ogbx_status st = use_device(device);
+  if (st != OGBX_OK) return st;
+
+  auto* e = new ogbx_maze_env();
+  e->device = device;
+  e->n = n_envs;
+  MazeParams& P = e->P;
+  std::memset(&P, 0, sizeof(P));
+  P.pm = make_point_model(4.0, 4.0);
+  P.H = spec->H;
+  P.W = spec->W;
+  P.num_tasks = spec->ntasks;
+  P.loco_type = opts->loco_type;
+  P.success_pre = opts->success_timing;
+  P.terminate_at_goal = opts->terminate_at_goal;
+  P.add_noise_to_goal = opts->add_noise_to_goal;
+  P.reward_task_id = opts->reward_task_id == 0 ? 1 : opts->reward_task_id;  // maze.py:361-362
+  if (opts->reward_task_id < 0) P.reward_task_id = -1;
+  P.max_steps = opts->max_episode_steps;
+  P.goal_tol = opts->loco_type == 0 ? 1.0 : 0.5;  // maze.py:86
+  for (int c = 0; c < spec->H * spec->W; ++c) P.wall[c] = spec->rows[c] == '1';
+  for (int t = 0; t < spec->ntasks; ++t)
+    for (int k = 0; k < 4; ++k) P.tasks[t][k] = spec->tasks[t][k];
+  if (std::strcmp(spec->name, "teleport") == 0) {  // maze.py:151-161
+    const int in_ij[2][2] = {{4, 6}, {5, 1}};
+    const int out_ij[3][2] = {{1, 7}, {6, 1}, {6, 10}};
+    P.n_tp_in = 2;
+    P.n_tp_out = 3;
+    P.tp_radius = 1.0;
+    for (int t = 0; t < 2; ++t) {
+      P.tp_in[t][0] = in_ij[t][1] * 4.0 - 4.0;
+      P.tp_in[t][1] = in_ij[t][0] * 4.0 - 4.0;
+    }
+    for (int t = 0; t < 3; ++t) {
+      P.tp_out[t][0] = out_ij[t][1] * 4.0 - 4.0;
+      P.tp_out[t][1] = out_ij[t][0] * 4.0 - 4.0;
+    }
+  }
+
+  const size_t n = (size_t)n_envs;
+  hipError_t herr = hipSuccess;
+  herr = hipMalloc(&e->S.qpos, n * 2 * sizeof(double));
+  if (herr == hipSuccess) herr = hipMalloc(&e->S.goal, n * 2 * sizeof(double));
+  if (herr == hipSuccess) herr = hipMalloc(&e->S.elapsed, n * sizeof(int32_t));
+  if (herr == hipSuccess) herr = hipMalloc(&e->S.task, n * sizeof(int32_t));
+  if (herr == hipSuccess) herr = hipMalloc(&e->S.episode, n * sizeof(uint32_t));
+  std::vector<int16_t> bfs;
+  build_bfs(P, bfs);
+  if (herr == hipSuccess) herr = hipMalloc(&e->Pd, sizeof(MazeParams));
+  if (herr == hipSuccess) herr = hipMemcpy(e->Pd, &P, sizeof(MazeParams), hipMemcpyHostToDevice);
+  if (herr == hipSuccess) herr = hipMalloc(&e->bfs, bfs.size() * sizeof(int16_t));
+  if (herr == hipSuccess)
+    herr = hipMemcpy(e->bfs, bfs.data(), bfs.size() * sizeof(int16_t), hipMemcpyHostToDevice);
+  if (herr == hipSuccess) herr = hipMemset(e->S.qpos, 0, n * 2 * sizeof(double));
+  if (herr == hipSuccess) herr = hipMemset(e->S.goal, 0, n * 2 * sizeof(double));
+  if (herr == hipSuccess) herr = hipMemset(e->S.elapsed, 0, n * sizeof(int32_t));
+  if (herr == hipSuccess) herr = hipMemset(e->S.task, 0, n * sizeof(int32_t));
+  if (herr == hipSuccess) herr = hipMemset(e->S.episode, 0, n * sizeof(uint32_t));
+  if (herr == hipSuccess) herr = hipDeviceSynchronize();
+  if (herr != hipSuccess) {
+    ogbx_maze_destroy(e);
+    return hip_fail(herr, "ogbx_maze_create: device allocation");
+  }
+  *out = e;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_destroy(ogbx_maze_t e) {
+  if (e == nullptr) return OGBX_OK;
+  hipSetDevice(e->device);
+  hipFree(e->S.qpos);
+  hipFree(e->S.goal);
+  hipFree(e->S.elapsed);
+  hipFree(e->S.task);
+  hipFree(e->S.episode);
+  hipFree(e->bfs);
+  hipFree(e->Pd);
+  delete e;
+  return OGBX_OK;
+}
+
+int64_t ogbx_maze_num_envs(ogbx_maze_t e) { return e ? e->n : 0; }
+
+ogbx_status ogbx_maze_static_tables(const char* maze_type, int32_t* map_h, int32_t* map_w,
+                                    int32_t* num_tasks, int32_t* map_out, int32_t* tasks_out) {
+  OGBX_CHECK(maze_type != nullptr, OGBX_EINVAL, "null maze_type");
+  const MazeSpec* spec = nullptr;
+  for (const auto& s : kMazes)
+    if (std::strcmp(s.name, maze_type) == 0) spec = &s;
+  OGBX_CHECK(spec != nullptr, OGBX_EINVAL, std::string("Unknown maze type: ") + maze_type);
+  if (map_h) *map_h = spec->H;
+  if (map_w) *map_w = spec->W;
+  if (num_tasks) *num_tasks = spec->ntasks;
+  if (map_out)
+    for (int c = 0; c < spec->H * spec->W; ++c) map_out[c] = spec->rows[c] == '1';
+  if (tasks_out)
+    for (int t = 0; t < spec->ntasks; ++t)
+      for (int k = 0; k < 4; ++k) tasks_out[4 * t + k] = spec->tasks[t][k];
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_describe(ogbx_maze_t e, int32_t* map_h, int32_t* map_w, int32_t* num_tasks,
+                               double* goal_tol, double* maze_unit) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  if (map_h) *map_h = e->P.H;
+  if (map_w) *map_w = e->P.W;
+  if (num_tasks) *num_tasks = e->P.num_tasks;
+  if (goal_tol) *goal_tol = e->P.goal_tol;
+  if (maze_unit) *maze_unit = e->P.pm.unit;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_tables(ogbx_maze_t e, int32_t* map_out, int32_t* tasks_out) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  if (map_out)
+    for (int c = 0; c < e->P.H * e->P.W; ++c) map_out[c] = e->P.wall[c];
+  if (tasks_out)
+    for (int t = 0; t < e->P.num_tasks; ++t)
+      for (int k = 0; k < 4; ++k) tasks_out[4 * t + k] = e->P.tasks[t][k];
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_reset(ogbx_maze_t e, const int32_t* task_id, const double* task_xy,
+                            const uint8_t* mask, const double* noise, double* obs, double* goal,
+                            uint64_t seed, void* stream) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(obs != nullptr && goal != nullptr, OGBX_EINVAL, "ogbx_maze_reset: null output");
+  OGBX_HIP(hipSetDevice(e->device));
+  e->seed = seed;
+  uint32_t k0, k1;
+  seed_key(seed, kTagMazeReset, &k0, &k1);
+  hipLaunchKernelGGL(maze_reset_kernel, dim3(grid_for(e->n, 256)), dim3(256), 0,
+                     (hipStream_t)stream, e->Pd, e->S, e->n, task_id, task_xy, mask, noise, obs,
+                     goal, k0, k1);
+  OGBX_LAUNCHED("maze_reset_kernel");
+  e->was_reset = true;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_f64,
+                           int32_t k_steps, double* obs, float* reward, uint8_t* terminated,
+                           uint8_t* truncated, uint8_t* success, double* final_obs,
+                           int32_t auto_reset, void* stream) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
+  OGBX_CHECK(e->P.loco_type == 0, OGBX_EINVAL,
+             "only the point-mass dynamics are implemented (ant/humanoid are wrapper-only)");
+  OGBX_CHECK(action && obs && reward && terminated && truncated && success, OGBX_EINVAL,
+             "ogbx_maze_step: null argument");
+  OGBX_CHECK(k_steps >= 1, OGBX_EINVAL, "k_steps must be >= 1");
+  OGBX_HIP(hipSetDevice(e->device));
+  uint32_t k0, k1;
+  seed_key(e->seed, kTagMazeReset, &k0, &k1);
+  dim3 grid(grid_for(e->n, 256)), block(256);
+  if (action_is_f64)
+    hipLaunchKernelGGL(maze_step_kernel<true>, grid, block, 0, (hipStream_t)stream, e->Pd, e->S,
+                       e->n, action, k_steps, obs, reward, terminated, truncated, success,
+                       final_obs, auto_reset, k0, k1);
+  else
+    hipLaunchKernelGGL(maze_step_kernel<false>, grid, block, 0, (hipStream_t)stream, e->Pd, e->S,
+                       e->n, action, k_steps, obs, reward, terminated, truncated, success,
+                       final_obs, auto_reset, k0, k1);
+  OGBX_LAUNCHED("maze_step_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_state(ogbx_maze_t e, double** qpos, double** goal_xy, int32_t** elapsed,
+                            int32_t** task_id) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  if (qpos) *qpos = e->S.qpos;
+  if (goal_xy) *goal_xy = e->S.goal;
+  if (elapsed) *elapsed = e->S.elapsed;
+  if (task_id) *task_id = e->S.task;
+  // A restore through these pointers counts as a reset.
+  e->was_reset = true;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_point_physics(ogbx_maze_t e, const double* qpos_in, const void* action,
+                               int32_t action_is_f64, int64_t n, double* qpos_out,
+                               uint8_t* contact_out, void* stream) {
+  OGBX_CHECK(e != nullptr && qpos_in && action && qpos_out, OGBX_EINVAL, "null argument");
+  if (n <= 0) return OGBX_OK;
+  OGBX_HIP(hipSetDevice(e->device));
+  dim3 grid(grid_for(n, 256)), block(256);
+  if (action_is_f64)
+    hipLaunchKernelGGL(point_physics_kernel<true>, grid, block, 0, (hipStream_t)stream, e->Pd,
+                       qpos_in, action, n, qpos_out, contact_out);
+  else
+    hipLaunchKernelGGL(point_physics_kernel<false>, grid, block, 0, (hipStream_t)stream, e->Pd,
+                       qpos_in, action, n, qpos_out, contact_out);
+  OGBX_LAUNCHED("point_physics_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_xy_to_ij(ogbx_maze_t e, const double* xy, int64_t n, int32_t* ij,
+                               void* stream) {
+  OGBX_CHECK(e != nullptr && xy && ij, OGBX_EINVAL, "null argument");
+  if (n <= 0) return OGBX_OK;
+  OGBX_HIP(hipSetDevice(e->device));
+  hipLaunchKernelGGL(xy_to_ij_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     e->Pd, xy, n, ij);
+  OGBX_LAUNCHED("xy_to_ij_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_ij_to_xy(ogbx_maze_t e, const int32_t* ij, int64_t n, double* xy,
+                               void* stream) {
+  OGBX_CHECK(e != nullptr && xy && ij, OGBX_EINVAL, "null argument");
+  if (n <= 0) return OGBX_OK;
+  OGBX_HIP(hipSetDevice(e->device));
+  hipLaunchKernelGGL(ij_to_xy_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                     e->Pd, ij, n, xy);
+  OGBX_LAUNCHED("ij_to_xy_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_oracle_subgoal(ogbx_maze_t e, const double* start_xy, const double* goal_xy,
+                                     int64_t n, double* subgoal_xy, void* stream) {
+  OGBX_CHECK(e != nullptr && start_xy && goal_xy && subgoal_xy, OGBX_EINVAL, "null argument");
+  if (n <= 0) return OGBX_OK;
+  OGBX_HIP(hipSetDevice(e->device));
+  hipLaunchKernelGGL(oracle_subgoal_kernel, dim3(grid_for(n, 256)), dim3(256), 0,
+                     (hipStream_t)stream, e->Pd, e->bfs, start_xy, goal_xy, n, subgoal_xy);
+  OGBX_LAUNCHED("oracle_subgoal_kernel");
+  return OGBX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,346 @@
+// point_physics.h -- device restatement of one PointEnv physics step:
+//   qpos <- qpos + 0.2*action ; qvel <- 0 ; mj_step x5 (RK4, dt 0.02)
+// for the 2-DoF slide-joint sphere of ogbench/locomaze/assets/point.xml inside
+// the box walls that MazeEnv.update_tree adds (ogbench/locomaze/maze.py:225-239).
+//
+// Model (see DESIGN.md "Point-mass contact model" for every assumed MuJoCo
+// default; wall-contact parity is UNPINNED -- MuJoCo is absent here):
+//   * M = m*I2, m = density*4/3*pi*r^3 (point.xml:8,28), qacc_smooth = 0
+//     (ctrl never written, gravity orthogonal to both slide axes).
+//   * Contacts: sphere-floor (always active at dist = 0, J_normal = 0 in the
+//     slide space) and sphere-box for wall cells of the 3x3 neighbourhood;
+//     condim 3, pyramidal cone, mu = 1 -> edges J = Jn +- mu*Jt_k.
+//   * Soft constraint per edge: aref = -B*(J.v) - K*imp*dist, cost 1/2*D*r^2 on
+//     r = J.a - aref < 0, D = 1/R, R = max(mjMINVAL, (1-imp)/imp*diagApprox).
+//   * qacc = argmin 1/2 m|a|^2 + sum_edges cost; solved exactly (Newton with an
+//     exact piecewise-quadratic line search, stopping on a consistent piece).
+//   * RK4 tableau of mj_RungeKutta; mj_advance uses the B-weighted velocity.
+//
+// Because every edge has aref = -B*J.v - kp with the same B, the residual of an
+// edge is r = J.(a + B v) + kp.  The solver therefore works in u = a + B*v:
+//   minimise 1/2 m |u - B v|^2 + 1/2 Df |u|^2 + sum_e 1/2 w_e min(0, J_e.u + kp_e)^2
+// (the floor's four edges +-e_x, +-e_y at dist 0 sum to the Df term), and
+// returns a = u - B*v.  Per wall contact the edges are n+t, n-t (weight D) and
+// n (the two edges along the vertical tangent, weight 2D).
+//
+// Fast path: if the sphere does not touch a wall at qpos+0.2a, every RK stage
+// has v = 0, a = 0 and qpos is returned unchanged (+0.0, as mj_integratePos).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ogbx {
+
+struct PointModel {
+  double mass;        // m
+  double h;           // opt.timestep (0.02)
+  double B, K;        // solref-derived damping / stiffness
+  double diag;        // diagApprox of one pyramid edge
+  double D_floor;     // 1/R at imp(dist = 0) = solimp[0]
+  double imp_dmin, imp_dmax, imp_width, imp_mid, imp_power;
+  double radius;      // sphere radius 0.7
+  double sphere_z;    // sphere centre height 0.7
+  double box_cz, box_hz;  // wall box centre z / half height
+  double box_hxy;     // wall box half size in x and y (maze_unit/2)
+  double unit, off_x, off_y;
+  int32_t nsub;       // frame_skip (5)
+  int32_t pad_;
+};
+
+constexpr double kMinVal = 1e-15;  // mjMINVAL
+// A sphere in an empty cell touches at most 3 wall boxes; the 4th slot holds
+// the second pseudo-contact of a (pathological) contact through a box z face.
+constexpr int kMaxContacts = 4;
+
+struct Contacts {
+  int n;
+  double nx[kMaxContacts], ny[kMaxContacts];  // Jn: gradient of dist (slide dofs)
+  double tx[kMaxContacts], ty[kMaxContacts];  // slide projection of the horizontal tangent
+  double kp[kMaxContacts];                    // K*imp*dist
+  double w[kMaxContacts];                     // D = 1/R of one edge
+};
+
+// MuJoCo getimpedance(): sigmoid between dmin and dmax over |dist|/width.
+__device__ inline double impedance(const PointModel& pm, double dist) {
+  double x = dist / pm.imp_width;
+  if (x < 0) x = -x;
+  if (x >= 1.0) return pm.imp_dmax;
+  if (x <= 0.0) return pm.imp_dmin;
+  double y;
+  if (x <= pm.imp_mid) {
+    double a = 1.0 / pow(pm.imp_mid, pm.imp_power - 1.0);
+    y = a * pow(x, pm.imp_power);
+  } else {
+    double b = 1.0 / pow(1.0 - pm.imp_mid, pm.imp_power - 1.0);
+    y = 1.0 - b * pow(1.0 - x, pm.imp_power);
+  }
+  return pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
+}
+
+// Store one contact into slot `slot` (static predicated writes keep Contacts
+// in VGPRs).
+__device__ inline void add_contact(const PointModel& pm, Contacts& c, int slot, double dist,
+                                   double nx, double ny, double tx, double ty) {
+  double imp = impedance(pm, dist);
+  double R = (1.0 - imp) * pm.diag / imp;
+  if (R < kMinVal) R = kMinVal;
+  double D = 1.0 / R;
+  double kp = pm.K * imp * dist;
+#pragma unroll
+  for (int s = 0; s < kMaxContacts; ++s) {
+    if (s == slot) {
+      c.nx[s] = nx;
+      c.ny[s] = ny;
+      c.tx[s] = tx;
+      c.ty[s] = ty;
+      c.kp[s] = kp;
+      c.w[s] = D;
+    }
+  }
+}
+
+// Sphere vs. every wall box of the 3x3 neighbourhood (MuJoCo sphere-box
+// collision in the box frame; boxes are axis aligned, margin 0).  `wall` is the
+// map in LDS (row-major, 1 = wall).  Returns the number of contacts.
+__device__ inline int collide_walls(const PointModel& pm, const uint8_t* wall, int H, int W,
+                                    double x, double y, Contacts& c) {
+#pragma unroll
+  for (int s = 0; s < kMaxContacts; ++s) {
+    c.nx[s] = 0.0; c.ny[s] = 0.0; c.tx[s] = 0.0; c.ty[s] = 0.0; c.kp[s] = 0.0; c.w[s] = 0.0;
+  }
+  const int i0 = (int)floor((y + pm.off_y + 0.5 * pm.unit) / pm.unit);
+  const int j0 = (int)floor((x + pm.off_x + 0.5 * pm.unit) / pm.unit);
+  const double dz = pm.sphere_z - pm.box_cz;
+  const double hx = pm.box_hxy, hz = pm.box_hz;
+  int nc = 0;
+#pragma unroll 1
+  for (int nb = 0; nb < 9; ++nb) {
+    const int i = i0 + nb / 3 - 1, j = j0 + nb % 3 - 1;
+    const bool is_wall = i >= 0 && i < H && j >= 0 && j < W && wall[i * W + j];
+    if (!is_wall || nc >= kMaxContacts) continue;
+    const double px = x - (j * pm.unit - pm.off_x);
+    const double py = y - (i * pm.unit - pm.off_y);
+    const double pz = dz;
+    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
+    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    const double clz = pz < -hz ? -hz : (pz > hz ? hz : pz);
+    const double tx = clx - px, ty = cly - py, tz = clz - pz;
+    const double d = sqrt(tx * tx + ty * ty + tz * tz);
+    if (d - pm.radius > 0.0) continue;
+    if (d > kMinVal) {
+      // centre outside the box: normal along (centre - closest point).
+      const double nx = -tx / d, ny = -ty / d;
+      add_contact(pm, c, nc, d - pm.radius, nx, ny, -ny, nx);
+    } else {
+      // centre inside the box: push out through the nearest face
+      // (faces ordered -x, +x, -y, +y, -z, +z; first strict minimum wins).
+      const double f0 = hx + px, f1 = hx - px, f2 = hx + py, f3 = hx - py, f4 = hz + pz,
+                   f5 = hz - pz;
+      int k = 0;
+      double best = f0;
+      if (f1 < best) { best = f1; k = 1; }
+      if (f2 < best) { best = f2; k = 2; }
+      if (f3 < best) { best = f3; k = 3; }
+      if (f4 < best) { best = f4; k = 4; }
+      if (f5 < best) { best = f5; k = 5; }
+      const double dist = -best - pm.radius;
+      const double sgn = (k & 1) ? 1.0 : -1.0;
+      if (k < 2) {
+        add_contact(pm, c, nc, dist, sgn, 0.0, 0.0, 1.0);
+      } else if (k < 4) {
+        add_contact(pm, c, nc, dist, 0.0, sgn, 1.0, 0.0);
+      } else {
+        // z face: Jn = 0, tangents e_x and e_y -> two pseudo-contacts.
+        add_contact(pm, c, nc, dist, 0.0, 0.0, 1.0, 0.0);
+        if (nc + 1 < kMaxContacts) add_contact(pm, c, ++nc, dist, 0.0, 0.0, 0.0, 1.0);
+      }
+    }
+    ++nc;
+  }
+  c.n = nc;
+  return nc;
+}
+
+// Edge e of contact s at u, with a = n.u + kp and b = t.u:
+//   e0: r = a + b (weight w), e1: r = a - b (w), e2: r = a (2w).
+
+// qacc for the given contacts at velocity (vx, vy).  See the header comment for
+// the u = a + B v formulation.  Loops run to the compile-time bound with an
+// `s < n` guard so nothing is dynamically indexed (no scratch).
+__device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
+                                 double* ax_out, double* ay_out) {
+  const double m = pm.mass, Df = pm.D_floor;
+  const double mf = m + Df;
+  const double bvx = pm.B * vx, bvy = pm.B * vy;
+  const int n = c.n;
+  // floor-only minimiser: u = m B v / (m + Df)
+  double ux = (m * bvx) / mf;
+  double uy = (m * bvy) / mf;
+  if (n > 0) {
+    for (int it = 0; it < 24; ++it) {
+      // gradient / Hessian of the current piece
+      const double gfx = m * (ux - bvx) + Df * ux;
+      const double gfy = m * (uy - bvy) + Df * uy;
+      double gx = gfx, gy = gfy, h00 = mf, h01 = 0.0, h11 = mf;
+      uint32_t act = 0;
+#pragma unroll
+      for (int s = 0; s < kMaxContacts; ++s) {
+        if (s < n) {
+          const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
+          const double b = c.tx[s] * ux + c.ty[s] * uy;
+          const double w = c.w[s];
+#pragma unroll
+          for (int e = 0; e < 3; ++e) {
+            const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
+            const double we = e == 2 ? 2.0 * w : w;
+            const double r = e == 2 ? a : a + sg * b;
+            if (r < 0.0) {
+              const double jx = e == 2 ? c.nx[s] : c.nx[s] + sg * c.tx[s];
+              const double jy = e == 2 ? c.ny[s] : c.ny[s] + sg * c.ty[s];
+              act |= 1u << (3 * s + e);
+              gx += we * r * jx;
+              gy += we * r * jy;
+              h00 += we * jx * jx;
+              h01 += we * jx * jy;
+              h11 += we * jy * jy;
+            }
+          }
+        }
+      }
+      if (gx == 0.0 && gy == 0.0) break;
+      const double det = h00 * h11 - h01 * h01;
+      const double px = -(h11 * gx - h01 * gy) / det;
+      const double py = -(h00 * gy - h01 * gx) / det;
+
+      // exact line search on phi(alpha) = f(u + alpha p): walk the edge
+      // breakpoints in increasing alpha until phi' changes sign.
+      double brk[3 * kMaxContacts];
+      uint32_t flag = 0, cross = 0;
+#pragma unroll
+      for (int s = 0; s < kMaxContacts; ++s) {
+        const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
+        const double b = c.tx[s] * ux + c.ty[s] * uy;
+        const double qa = c.nx[s] * px + c.ny[s] * py;
+        const double qb = c.tx[s] * px + c.ty[s] * py;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          const int k = 3 * s + e;
+          const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
+          const double r = e == 2 ? a : a + sg * b;
+          const double q = e == 2 ? qa : qa + sg * qb;
+          brk[k] = INFINITY;
+          if (s < n) {
+            if (r < 0.0 || (r == 0.0 && q < 0.0)) flag |= 1u << k;
+            if ((r < 0.0 && q > 0.0) || (r > 0.0 && q < 0.0)) {
+              brk[k] = -r / q;
+              cross |= 1u << k;
+            }
+          }
+        }
+      }
+      const uint32_t flag0 = flag;
+      const double base0 = px * gfx + py * gfy;
+      const double base1 = mf * (px * px + py * py);
+      double alpha = 0.0;
+      bool crossed = false;
+      for (int seg = 0; seg <= 3 * kMaxContacts; ++seg) {
+        double c0 = base0, c1 = base1, beta = INFINITY;
+#pragma unroll
+        for (int s = 0; s < kMaxContacts; ++s) {
+          const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
+          const double b = c.tx[s] * ux + c.ty[s] * uy;
+          const double qa = c.nx[s] * px + c.ny[s] * py;
+          const double qb = c.tx[s] * px + c.ty[s] * py;
+#pragma unroll
+          for (int e = 0; e < 3; ++e) {
+            const int k = 3 * s + e;
+            if (flag & (1u << k)) {
+              const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
+              const double we = e == 2 ? 2.0 * c.w[s] : c.w[s];
+              const double r = e == 2 ? a : a + sg * b;
+              const double q = e == 2 ? qa : qa + sg * qb;
+              c0 += we * q * r;
+              c1 += we * q * q;
+            }
+            if ((cross & (1u << k)) && brk[k] < beta) beta = brk[k];
+          }
+        }
+        const double ac = -c0 / c1;
+        if (ac <= beta) {
+          alpha = ac;
+          break;
+        }
+        alpha = beta;
+        crossed = true;
+#pragma unroll
+        for (int k = 0; k < 3 * kMaxContacts; ++k)
+          if ((cross & (1u << k)) && brk[k] == beta) {
+            flag ^= 1u << k;
+            cross &= ~(1u << k);
+          }
+      }
+      ux += alpha * px;
+      uy += alpha * py;
+      if (!crossed && flag0 == act) break;  // exact minimiser of a consistent piece
+    }
+  }
+  *ax_out = ux - bvx;
+  *ay_out = uy - bvy;
+}
+
+// One PointEnv step starting from qpos + delta with qvel = 0.  Returns 1 if a
+// wall contact was present at the start (slow path taken).
+// The 5 substeps x 4 RK stages run as one loop of 20 force evaluations so the
+// solver is instantiated once (mj_step -> mj_forward + mj_RungeKutta(N=4),
+// RK4_A = {1/2 ; 0, 1/2 ; 0, 0, 1}, RK4_B = {1/6, 1/3, 1/3, 1/6}).
+__device__ inline int point_step(const PointModel& pm, const uint8_t* wall, int H, int W,
+                                 double* px, double* py) {
+  double x = *px, y = *py;
+  Contacts c;
+  if (collide_walls(pm, wall, H, W, x, y, c) == 0) {
+    *px = x + 0.0;
+    *py = y + 0.0;
+    return 0;
+  }
+  const double h = pm.h;
+  double vx = 0.0, vy = 0.0;                          // X[0] velocity of the substep
+  double qsx = x, qsy = y, vsx = 0.0, vsy = 0.0;      // state of the current RK stage
+  double sqx = 0.0, sqy = 0.0, svx = 0.0, svy = 0.0;  // B-weighted sums (dX)
+  const int nstage = 4 * pm.nsub;
+#pragma unroll 1
+  for (int e = 0; e < nstage; ++e) {
+    const int st = e & 3;
+    double fx, fy;
+    if (e != 0) collide_walls(pm, wall, H, W, qsx, qsy, c);
+    solve_acc(pm, c, vsx, vsy, &fx, &fy);
+    const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
+    sqx = sqx + b * vsx;
+    sqy = sqy + b * vsy;
+    svx = svx + b * fx;
+    svy = svy + b * fy;
+    if (st < 3) {
+      const double cf = (st < 2) ? 0.5 : 1.0;
+      qsx = x + h * (cf * vsx);
+      qsy = y + h * (cf * vsy);
+      vsx = vx + (cf * fx) * h;
+      vsy = vy + (cf * fy) * h;
+    } else {
+      // mj_advance: qvel += h*dX_acc ; qpos += h*dX_vel
+      vx = vx + svx * h;
+      vy = vy + svy * h;
+      x = x + h * sqx;
+      y = y + h * sqy;
+      qsx = x;
+      qsy = y;
+      vsx = vx;
+      vsy = vy;
+      sqx = sqy = svx = svy = 0.0;
+    }
+  }
+  *px = x;
+  *py = y;
+  return 1;
+}
+
+}  // namespace ogbx

@@ -1,0 +1,492 @@
+"""Batched locomaze (pointmaze) environments on MI355X.
+
+``MazeEnv`` is the batched counterpart of the reference ``make_maze_env(...)``
+class (ogbench/locomaze/maze.py:13-567): the same constructor options, task
+tables, ``reset(options=...)``/``step(action)`` semantics and helper methods,
+but every env of the batch lives in HBM and one ``step`` is one HIP launch
+(``ogbx_maze_step`` in libogbx).  Tensors are PyTorch-ROCm tensors with a
+leading batch dimension N.
+
+Differences that follow from batching (documented in DESIGN.md):
+  * returned tensors are views of env-owned buffers that the next ``step``
+    overwrites (clone them to keep them);
+  * ``info['success']``, ``terminated`` and ``truncated`` are bool tensors;
+  * with ``auto_reset=True`` finished envs are reset inside the same step
+    (gymnasium same-step autoreset); ``info['final_observation']`` then holds
+    the terminal observation;
+  * reset noise comes from a counter-based Philox stream keyed by ``seed``
+    (the reference draws np.random.uniform), and can be injected exactly with
+    ``options['noise']`` for parity tests.
+"""
+
+from __future__ import annotations
+
+import re
+
+import numpy as np
+
+from . import _lib
+from .spaces import Box
+
+LOCO_TYPES = {'point': 0, 'ant': 1, 'humanoid': 2}
+MAZE_TYPES = ('arena', 'medium', 'large', 'giant', 'teleport')
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _resolve_device(device):
+    torch = _torch()
+    if device is None:
+        device = 'cuda'
+    device = torch.device(device)
+    if device.type != 'cuda':
+        raise RuntimeError('ogbench_amd envs run on the GPU only (no CPU fallback); got device %s' % device)
+    if device.index is None:
+        device = torch.device('cuda', torch.cuda.current_device())
+    return device
+
+
+def static_tables(maze_type):
+    """(maze_map int32[H,W], tasks int32[T,4]) without touching the GPU."""
+    L = _lib.lib()
+    H, W, T = _lib.c_int32(), _lib.c_int32(), _lib.c_int32()
+    _lib.check(L.ogbx_maze_static_tables(maze_type.encode(), H, W, T, None, None))
+    mp = np.zeros((H.value, W.value), np.int32)
+    tk = np.zeros((T.value, 4), np.int32)
+    _lib.check(
+        L.ogbx_maze_static_tables(
+            maze_type.encode(), H, W, T, mp.ctypes.data_as(_lib.c_void_p), tk.ctypes.data_as(_lib.c_void_p)
+        )
+    )
+    return mp, tk
+
+
+class MazeEnv:
+    """Batch of ``num_envs`` maze environments (reference: maze.py:31-567)."""
+
+    def __init__(
+        self,
+        loco_env_type='point',
+        maze_type='large',
+        num_envs=1,
+        device=None,
+        maze_unit=4.0,
+        maze_height=0.5,
+        terminate_at_goal=True,
+        success_timing='post',
+        ob_type='states',
+        add_noise_to_goal=True,
+        reward_task_id=None,
+        use_oracle_rep=False,
+        max_episode_steps=1000,
+        auto_reset=False,
+        seed=None,
+    ):
+        if loco_env_type not in LOCO_TYPES:
+            raise ValueError(f'Unknown locomotion environment type: {loco_env_type}')
+        if maze_type not in MAZE_TYPES:
+            raise ValueError(f'Unknown maze type: {maze_type}')
+        assert ob_type in ['states', 'pixels']
+        assert success_timing in ['pre', 'post']
+        if ob_type == 'pixels':
+            raise NotImplementedError('pixel observations (MuJoCo rendering) are out of scope')
+        if maze_unit != 4.0 or maze_height != 0.5:
+            raise NotImplementedError('only the registered maze_unit=4.0 / maze_height=0.5 are supported')
+        torch = _torch()
+        self.device = _resolve_device(device)
+        self.num_envs = int(num_envs)
+        self._loco_env_type = loco_env_type
+        self._maze_type = maze_type
+        self._maze_unit = maze_unit
+        self._maze_height = maze_height
+        self._terminate_at_goal = terminate_at_goal
+        self._success_timing = success_timing
+        self._ob_type = ob_type
+        self._add_noise_to_goal = add_noise_to_goal
+        self._reward_task_id = reward_task_id
+        self._use_oracle_rep = use_oracle_rep
+        self._offset_x = 4
+        self._offset_y = 4
+        self._noise = 1
+        self._goal_tol = 1.0 if loco_env_type == 'point' else 0.5
+        self.max_episode_steps = int(max_episode_steps)
+        self.auto_reset = bool(auto_reset)
+
+        opts = _lib.MazeOpts(
+            loco_type=LOCO_TYPES[loco_env_type],
+            success_timing=0 if success_timing == 'post' else 1,
+            terminate_at_goal=int(bool(terminate_at_goal)),
+            add_noise_to_goal=int(bool(add_noise_to_goal)),
+            reward_task_id=-1 if reward_task_id is None else int(reward_task_id),
+            max_episode_steps=self.max_episode_steps,
+        )
+        L = _lib.lib()
+        h = _lib.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(L.ogbx_maze_create(maze_type.encode(), self.num_envs, self.device.index, opts, h))
+        self._h = h
+        self._L = L
+
+        self.maze_map, tasks = static_tables(maze_type)
+        self.task_infos = []
+        for i, t in enumerate(tasks):
+            init_ij, goal_ij = (int(t[0]), int(t[1])), (int(t[2]), int(t[3]))
+            self.task_infos.append(
+                dict(
+                    task_name=f'task{i + 1}',
+                    init_ij=init_ij,
+                    init_xy=self.ij_to_xy(init_ij),
+                    goal_ij=goal_ij,
+                    goal_xy=self.ij_to_xy(goal_ij),
+                )
+            )
+        self.num_tasks = len(self.task_infos)
+        if self._reward_task_id == 0:
+            self._reward_task_id = 1  # Default task (maze.py:361-362).
+
+        ob_dim = 2 if loco_env_type == 'point' else (29 if loco_env_type == 'ant' else 69)
+        act_dim = 2 if loco_env_type == 'point' else (8 if loco_env_type == 'ant' else 21)
+        self.single_observation_space = Box(-np.inf, np.inf, (ob_dim,), np.float64)
+        self.single_action_space = Box(-1.0, 1.0, (act_dim,), np.float32)
+        self.observation_space = Box(-np.inf, np.inf, (self.num_envs, ob_dim), np.float64)
+        self.action_space = Box(-1.0, 1.0, (self.num_envs, act_dim), np.float32)
+
+        n = self.num_envs
+        kw = dict(device=self.device)
+        self._obs = torch.zeros(n, 2, dtype=torch.float64, **kw)
+        self._goal = torch.zeros(n, 2, dtype=torch.float64, **kw)
+        self._final_obs = torch.zeros(n, 2, dtype=torch.float64, **kw)
+        self._reward = torch.zeros(n, dtype=torch.float32, **kw)
+        self._term = torch.zeros(n, dtype=torch.uint8, **kw)
+        self._trunc = torch.zeros(n, dtype=torch.uint8, **kw)
+        self._succ = torch.zeros(n, dtype=torch.uint8, **kw)
+        self._seed = None
+        self._init_seed = seed
+        self._has_reset = False
+        self.cur_task_id = None
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, '_h', None) is not None and self._h.value:
+            self._L.ogbx_maze_destroy(self._h)
+            self._h = _lib.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def unwrapped(self):
+        return self
+
+    def _stream(self):
+        return _lib.stream_of(self.device)
+
+    # ------------------------------------------------------------ helpers
+    def xy_to_ij(self, xy):
+        """maze.py:552-556 (Python int() truncation).  Scalars or [n,2] tensors."""
+        if isinstance(xy, (tuple, list)) or (isinstance(xy, np.ndarray) and xy.ndim == 1):
+            maze_unit = self._maze_unit
+            i = int((xy[1] + self._offset_y + 0.5 * maze_unit) / maze_unit)
+            j = int((xy[0] + self._offset_x + 0.5 * maze_unit) / maze_unit)
+            return i, j
+        torch = _torch()
+        xy = xy.to(self.device, torch.float64).contiguous()
+        ij = torch.empty(xy.shape[0], 2, dtype=torch.int32, device=self.device)
+        _lib.check(self._L.ogbx_maze_xy_to_ij(self._h, _lib.ptr(xy), xy.shape[0], _lib.ptr(ij), self._stream()))
+        return ij
+
+    def ij_to_xy(self, ij):
+        """maze.py:558-562."""
+        if isinstance(ij, (tuple, list)) or (isinstance(ij, np.ndarray) and ij.ndim == 1):
+            i, j = ij
+            x = j * self._maze_unit - self._offset_x
+            y = i * self._maze_unit - self._offset_y
+            return x, y
+        torch = _torch()
+        ij = ij.to(self.device, torch.int32).contiguous()
+        xy = torch.empty(ij.shape[0], 2, dtype=torch.float64, device=self.device)
+        _lib.check(self._L.ogbx_maze_ij_to_xy(self._h, _lib.ptr(ij), ij.shape[0], _lib.ptr(xy), self._stream()))
+        return xy
+
+    def get_oracle_subgoal(self, start_xy, goal_xy):
+        """Batched maze.py:503-550: BFS next-hop subgoal for each (start, goal) pair."""
+        torch = _torch()
+        s = start_xy.to(self.device, torch.float64).contiguous()
+        g = goal_xy.to(self.device, torch.float64).contiguous()
+        out = torch.empty_like(s)
+        _lib.check(
+            self._L.ogbx_maze_oracle_subgoal(
+                self._h, _lib.ptr(s), _lib.ptr(g), s.shape[0], _lib.ptr(out), self._stream()
+            )
+        )
+        return out
+
+    def _state_ptrs(self):
+        q, g, e, t = _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p()
+        _lib.check(self._L.ogbx_maze_state(self._h, q, g, e, t))
+        return q.value, g.value, e.value, t.value
+
+    def _state_views(self):
+        """torch views of the env-owned state (qpos, goal, elapsed, task)."""
+        torch = _torch()
+        q, g, e, t = self._state_ptrs()
+        n = self.num_envs
+
+        return (
+            _from_ptr(q, (n, 2), torch.float64, self.device),
+            _from_ptr(g, (n, 2), torch.float64, self.device),
+            _from_ptr(e, (n,), torch.int32, self.device),
+            _from_ptr(t, (n,), torch.int32, self.device),
+        )
+
+    def get_xy(self):
+        return self._state_views()[0].clone()
+
+    @property
+    def cur_goal_xy(self):
+        return self._state_views()[1].clone()
+
+    def state_dict(self):
+        q, g, e, t = self._state_views()
+        return dict(qpos=q.clone(), goal=g.clone(), elapsed=e.clone(), task=t.clone(), seed=self._seed)
+
+    def load_state_dict(self, sd):
+        q, g, e, t = self._state_views()
+        q.copy_(sd['qpos'])
+        g.copy_(sd['goal'])
+        e.copy_(sd['elapsed'])
+        t.copy_(sd['task'])
+        if sd.get('seed') is not None:
+            self._seed = int(sd['seed'])
+        self._has_reset = True
+
+    # ------------------------------------------------------------ reset/step
+    def _task_tensor(self, task_id):
+        torch = _torch()
+        if isinstance(task_id, (int, np.integer)):
+            assert 1 <= task_id <= self.num_tasks, f'Task ID must be in [1, {self.num_tasks}].'
+            return torch.full((self.num_envs,), int(task_id), dtype=torch.int32, device=self.device)
+        t = torch.as_tensor(task_id).to(self.device, torch.int32).reshape(-1).contiguous()
+        assert t.numel() == self.num_envs, 'task_id tensor must have one entry per env'
+        lo, hi = int(t.min()), int(t.max())
+        assert 1 <= lo and hi <= self.num_tasks, f'Task ID must be in [1, {self.num_tasks}].'
+        return t
+
+    def _task_xy_tensor(self, task_info):
+        torch = _torch()
+        if isinstance(task_info, dict):
+            ix, iy = self.ij_to_xy(task_info['init_ij'])
+            gx, gy = self.ij_to_xy(task_info['goal_ij'])
+            row = torch.tensor([ix, iy, gx, gy], dtype=torch.float64, device=self.device)
+            return row.expand(self.num_envs, 4).contiguous()
+        t = torch.as_tensor(task_info).to(self.device, torch.float64).contiguous()
+        assert t.shape == (self.num_envs, 4), 'task_info tensor must be [num_envs, 4] (init_xy, goal_xy)'
+        return t
+
+    def reset(self, *, seed=None, options=None, mask=None):
+        """MazeEnv.reset (maze.py:373-431) for every env (or those in ``mask``).
+
+        options: ``task_id`` (int or [N] tensor), ``task_info`` (dict with
+        init_ij/goal_ij, or an [N,4] xy tensor), ``noise`` ([N,4] injected
+        uniform(-1,1) draws; test hook), ``render_goal`` (unsupported).
+        Returns (obs [N,2] f64, {'goal': [N,2] f64}).
+        """
+        torch = _torch()
+        options = {} if options is None else options
+        if options.get('render_goal'):
+            raise NotImplementedError('render_goal needs MuJoCo rendering (out of scope)')
+        if seed is not None:
+            self._seed = int(seed) & ((1 << 64) - 1)
+        elif self._seed is None:
+            self._seed = (
+                int(self._init_seed) if self._init_seed is not None else int(np.random.randint(0, 2**63 - 1))
+            )
+        task_t = task_xy = None
+        if self._reward_task_id is not None:
+            self.cur_task_id = self._reward_task_id
+        elif 'task_id' in options:
+            task_t = self._task_tensor(options['task_id'])
+            self.cur_task_id = options['task_id'] if isinstance(options['task_id'], int) else None
+        elif 'task_info' in options:
+            task_xy = self._task_xy_tensor(options['task_info'])
+            task_t = torch.ones(self.num_envs, dtype=torch.int32, device=self.device)
+            self.cur_task_id = None
+        else:
+            self.cur_task_id = None  # drawn per env on the device
+        noise = options.get('noise')
+        if noise is not None:
+            noise = torch.as_tensor(noise).to(self.device, torch.float64).contiguous()
+            assert noise.shape == (self.num_envs, 4)
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask).to(self.device, torch.uint8).contiguous()
+        _lib.check(
+            self._L.ogbx_maze_reset(
+                self._h,
+                _lib.ptr(task_t),
+                _lib.ptr(task_xy),
+                _lib.ptr(m),
+                _lib.ptr(noise),
+                _lib.ptr(self._obs),
+                _lib.ptr(self._goal),
+                self._seed,
+                self._stream(),
+            ),
+            'reset',
+        )
+        self._has_reset = True
+        return self._obs, {'goal': self._goal}
+
+    def _action(self, action):
+        torch = _torch()
+        if not isinstance(action, torch.Tensor):
+            action = torch.as_tensor(np.asarray(action))
+        if action.device != self.device:
+            action = action.to(self.device)
+        if action.dtype not in (torch.float32, torch.float64):
+            action = action.to(torch.float32)
+        if not action.is_contiguous():
+            action = action.contiguous()
+        return action
+
+    def step(self, action):
+        """One env step of all envs (maze.py:433-466 + point.py:64-95 + TimeLimit).
+
+        action: [N,2] float32 (NEP-50 float32 scaling) or float64.
+        Returns (obs, reward, terminated, truncated, info) with info['success'].
+        """
+        a = self._action(action)
+        if a.shape != (self.num_envs, 2):
+            raise ValueError(f'action must have shape ({self.num_envs}, 2), got {tuple(a.shape)}')
+        _lib.check(
+            self._L.ogbx_maze_step(
+                self._h,
+                _lib.ptr(a),
+                int(a.dtype == _torch().float64),
+                1,
+                _lib.ptr(self._obs),
+                _lib.ptr(self._reward),
+                _lib.ptr(self._term),
+                _lib.ptr(self._trunc),
+                _lib.ptr(self._succ),
+                _lib.ptr(self._final_obs) if self.auto_reset else None,
+                int(self.auto_reset),
+                self._stream(),
+            ),
+            'step',
+        )
+        info = {'success': self._succ.view(_torch().bool)}
+        if self.auto_reset:
+            info['final_observation'] = self._final_obs
+        return self._obs, self._reward, self._term.view(_torch().bool), self._trunc.view(_torch().bool), info
+
+    def rollout(self, actions, out=None):
+        """K fused steps in ONE launch: actions [K,N,2] -> per-step outputs [K,N,...].
+
+        Equivalent to K calls of ``step`` with the same auto_reset setting.
+        """
+        torch = _torch()
+        a = self._action(actions)
+        K = a.shape[0]
+        if a.shape != (K, self.num_envs, 2):
+            raise ValueError(f'actions must have shape (K, {self.num_envs}, 2)')
+        if out is None:
+            kw = dict(device=self.device)
+            out = dict(
+                obs=torch.empty(K, self.num_envs, 2, dtype=torch.float64, **kw),
+                reward=torch.empty(K, self.num_envs, dtype=torch.float32, **kw),
+                terminated=torch.empty(K, self.num_envs, dtype=torch.uint8, **kw),
+                truncated=torch.empty(K, self.num_envs, dtype=torch.uint8, **kw),
+                success=torch.empty(K, self.num_envs, dtype=torch.uint8, **kw),
+            )
+        _lib.check(
+            self._L.ogbx_maze_step(
+                self._h,
+                _lib.ptr(a),
+                int(a.dtype == torch.float64),
+                K,
+                _lib.ptr(out['obs']),
+                _lib.ptr(out['reward']),
+                _lib.ptr(out['terminated']),
+                _lib.ptr(out['truncated']),
+                _lib.ptr(out['success']),
+                None,
+                int(self.auto_reset),
+                self._stream(),
+            ),
+            'rollout',
+        )
+        return out
+
+    def physics(self, qpos, action):
+        """Free-standing PointEnv physics (point.py:68-73) for [n,2] qpos/actions."""
+        torch = _torch()
+        q = qpos.to(self.device, torch.float64).contiguous()
+        a = self._action(action)
+        out = torch.empty_like(q)
+        contact = torch.empty(q.shape[0], dtype=torch.uint8, device=self.device)
+        _lib.check(
+            self._L.ogbx_point_physics(
+                self._h,
+                _lib.ptr(q),
+                _lib.ptr(a),
+                int(a.dtype == torch.float64),
+                q.shape[0],
+                _lib.ptr(out),
+                _lib.ptr(contact),
+                self._stream(),
+            )
+        )
+        return out, contact
+
+
+def _from_ptr(addr, shape, dtype, device):
+    """Non-owning torch view of device memory owned by libogbx."""
+    torch = _torch()
+    numel = int(np.prod(shape))
+    nbytes = numel * torch.empty((), dtype=dtype).element_size()
+    iface = {
+        'shape': tuple(shape),
+        'typestr': {torch.float64: '<f8', torch.int32: '<i4', torch.uint8: '|u1', torch.float32: '<f4'}[dtype],
+        'data': (addr, False),
+        'version': 3,
+        'strides': None,
+    }
+
+    class _Holder:
+        __cuda_array_interface__ = iface
+
+    t = torch.as_tensor(_Holder(), device=device)
+    assert t.numel() * t.element_size() == nbytes
+    return t
+
+
+# ---------------------------------------------------------------- registry
+_LOCO_MAX_STEPS = {'point': 1000, 'ant': 1000, 'humanoid': 2000}
+
+
+def parse_env_id(env_id):
+    """Registry entries of ogbench/locomaze/__init__.py:16-527 as kwargs."""
+    m = re.fullmatch(r'(visual-)?(point|ant|humanoid)maze-(arena|medium|large|giant|teleport)'
+                     r'(-singletask(?:-task(\d))?)?-v0', env_id)
+    if m is None:
+        return None
+    visual, loco, maze, single, task = m.groups()
+    if visual:
+        raise NotImplementedError(f'{env_id}: pixel observations are out of scope')
+    max_steps = _LOCO_MAX_STEPS[loco]
+    if loco == 'humanoid' and maze == 'giant':
+        max_steps = 4000
+    kwargs = dict(loco_env_type=loco, maze_type=maze, max_episode_steps=max_steps)
+    if single:
+        kwargs.update(
+            reward_task_id=0 if task is None else int(task), add_noise_to_goal=False, success_timing='pre'
+        )
+    return kwargs

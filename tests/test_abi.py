@@ -1,0 +1,56 @@
+"""CPU checks of the C-ABI boundary: libogbx.so loads, exports every symbol of
+include/ogbx.h, and its device-free tables match the reference fixtures."""
+
+import ctypes
+
+import numpy as np
+
+from ogbench_amd import _lib
+
+
+def test_library_loads_and_reports_abi():
+    L = _lib.lib()
+    assert L.ogbx_abi_version() == 1
+    assert L.ogbx_build_arch() == b'gfx950'
+
+
+def test_every_declared_symbol_is_exported():
+    L = _lib.lib()
+    declared = _lib.declared_symbols()
+    assert len(declared) >= 15
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert missing == []
+    # every symbol the Python layer binds is declared in the header
+    assert set(_lib._SIGNATURES) <= set(declared)
+
+
+def test_static_tables_match_reference(golden_locomaze):
+    from ogbench_amd.locomaze import static_tables
+
+    for name in ['arena', 'medium', 'large', 'giant', 'teleport']:
+        mp, tk = static_tables(name)
+        assert np.array_equal(mp, golden_locomaze[f'map_{name}'])
+        assert np.array_equal(tk, golden_locomaze[f'tasks_{name}'])
+
+
+def test_unknown_maze_type_is_value_error():
+    import pytest
+
+    from ogbench_amd.locomaze import static_tables
+
+    with pytest.raises(ValueError, match='Unknown maze type'):
+        static_tables('spiral')
+
+
+def test_create_without_gpu_fails_loudly():
+    """No CPU fallback: creating a handle without a gfx950 device must fail."""
+    import torch
+
+    if torch.cuda.is_available():
+        return
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    opts = _lib.MazeOpts(0, 0, 1, 1, -1, 1000)
+    st = L.ogbx_maze_create(b'large', 16, 0, opts, h)
+    assert st == _lib.OGBX_EDEVICE
+    assert 'CPU fallback' in _lib.last_error() or 'device' in _lib.last_error()

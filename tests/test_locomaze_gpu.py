@@ -1,0 +1,160 @@
+"""GPU parity: libogbx locomaze kernels (through the C-ABI) vs the oracle and the
+reference golden vectors.  Tolerances: bit-exact for indices, masks, reset
+arithmetic and free-space steps; 1e-9 abs for contact dynamics (north_star
+allows 1e-5; the oracle solves the same model with a different solver)."""
+
+import numpy as np
+import pytest
+import torch
+
+import ogbench_amd
+from oracle import locomaze as orc
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9
+
+
+def _env(gpu, n, maze='large', **kw):
+    return ogbench_amd.MazeEnv('point', maze, num_envs=n, device=gpu, **kw)
+
+
+def test_free_space_bit_exact(gpu, golden_locomaze):
+    q = torch.tensor(golden_locomaze['free_qpos'])
+    env = _env(gpu, 1)
+    for kind in ('32', '64'):
+        a = torch.tensor(golden_locomaze[f'free_act{kind}'])
+        out, contact = env.physics(q, a)
+        ref, rc = orc.physics('large', q.numpy(), a.numpy())
+        assert np.array_equal(contact.cpu().numpy(), rc)
+        free = rc == 0
+        assert free.sum() > 1000
+        assert np.array_equal(out.cpu().numpy()[free], golden_locomaze[f'free_out{kind}'][free])
+
+
+@pytest.mark.parametrize('maze', ['medium', 'large', 'giant', 'arena'])
+@pytest.mark.parametrize('f64', [False, True])
+def test_physics_matches_oracle_with_contacts(gpu, maze, f64):
+    rng = np.random.RandomState(hash((maze, f64)) % 2**31)
+    mp, _ = orc.tables(maze)
+    cells = np.argwhere(mp == 0)
+    n = 20000
+    c = cells[rng.randint(len(cells), size=n)]
+    # positions concentrated near walls: offsets up to 1.9 from the cell centre
+    q = np.stack([c[:, 1] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n), c[:, 0] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n)], 1)
+    a = rng.uniform(-1, 1, (n, 2)).astype(np.float64 if f64 else np.float32)
+    env = _env(gpu, 1, maze)
+    out, contact = env.physics(torch.tensor(q), torch.tensor(a))
+    ref, rc = orc.physics(maze, q, a, nthreads=8)
+    got = out.cpu().numpy()
+    assert np.array_equal(contact.cpu().numpy(), rc)
+    assert rc.mean() > 0.3  # the test really exercises contacts
+    assert np.abs(got - ref).max() <= TOL
+    assert np.array_equal(got[rc == 0], ref[rc == 0])
+
+
+def test_xy_to_ij_bit_exact(gpu, golden_locomaze):
+    env = _env(gpu, 1)
+    ij = env.xy_to_ij(torch.tensor(golden_locomaze['xy2ij_in']))
+    assert np.array_equal(ij.cpu().numpy(), golden_locomaze['xy2ij_out'])
+
+
+def test_success_mask_bit_exact(gpu, golden_locomaze):
+    pos, goal = golden_locomaze['succ_pos'], golden_locomaze['succ_goal']
+    n = len(pos)
+    env = _env(gpu, n, success_timing='pre')
+    env.reset(options=dict(task_id=1, noise=torch.zeros(n, 4, dtype=torch.float64)))
+    sd = env.state_dict()
+    sd['qpos'] = torch.tensor(pos)
+    sd['goal'] = torch.tensor(goal)
+    env.load_state_dict(sd)
+    _, _, _, _, info = env.step(torch.zeros(n, 2))
+    assert np.array_equal(info['success'].cpu().numpy(), golden_locomaze['succ_out'].astype(bool))
+
+
+@pytest.mark.parametrize('maze', ['medium', 'large'])
+def test_reset_with_injected_noise(gpu, golden_locomaze, maze):
+    tid = golden_locomaze[f'reset_{maze}_task']
+    noise = golden_locomaze[f'reset_{maze}_noise']
+    env = _env(gpu, len(tid), maze)
+    obs, info = env.reset(options=dict(task_id=torch.tensor(tid), noise=torch.tensor(noise)))
+    exp = golden_locomaze[f'reset_{maze}_out']
+    assert np.array_equal(obs.cpu().numpy(), exp[:, :2])
+    assert np.array_equal(info['goal'].cpu().numpy(), exp[:, 2:])
+
+
+@pytest.mark.parametrize('maze', ['medium', 'large', 'giant'])
+def test_oracle_subgoal_bit_exact(gpu, golden_locomaze, maze):
+    env = _env(gpu, 1, maze)
+    s = torch.tensor(golden_locomaze[f'subgoal_{maze}_start'])
+    g = torch.tensor(golden_locomaze[f'subgoal_{maze}_goal'])
+    out = env.get_oracle_subgoal(s, g)
+    assert np.array_equal(out.cpu().numpy(), golden_locomaze[f'subgoal_{maze}_out'])
+
+
+@pytest.mark.parametrize('fused', [False, True])
+def test_env_rollout_matches_oracle(gpu, fused):
+    """300 steps of N envs with auto-reset (Philox reset draws), vs the oracle."""
+    n, k = 4096, 300
+    env = _env(gpu, n, 'large', auto_reset=True, max_episode_steps=120)
+    rng = np.random.RandomState(7)
+    tid = (np.arange(n) % 5 + 1).astype(np.int32)
+    noise = rng.uniform(-1, 1, (n, 4))
+    seed = 0x1234_5678_9ABC
+    env.reset(seed=seed, options=dict(task_id=torch.tensor(tid), noise=torch.tensor(noise)))
+    st = orc.reset('large', tid, noise, max_steps=120)
+    # drive envs toward their goals part of the time so that successes happen
+    acts = rng.uniform(-1, 1, (k, n, 2)).astype(np.float32)
+    key = orc.philox_key(seed, orc.TAG_MAZE_RESET)
+    ref = orc.step('large', st, acts, auto_reset=1, key=key, nthreads=8)
+    if fused:
+        out = env.rollout(torch.tensor(acts))
+        got = {k2: v.cpu().numpy() for k2, v in out.items()}
+    else:
+        got = dict(obs=[], reward=[], terminated=[], truncated=[], success=[])
+        for t in range(k):
+            o, r, te, tr, info = env.step(torch.tensor(acts[t]))
+            got['obs'].append(o.cpu().numpy().copy())
+            got['reward'].append(r.cpu().numpy().copy())
+            got['terminated'].append(te.cpu().numpy().copy())
+            got['truncated'].append(tr.cpu().numpy().copy())
+            got['success'].append(info['success'].cpu().numpy().copy())
+        got = {k2: np.stack(v) for k2, v in got.items()}
+    assert np.abs(got['obs'] - ref['obs']).max() <= TOL
+    for key2 in ('terminated', 'truncated', 'success'):
+        assert np.array_equal(got[key2].astype(bool), ref[key2].astype(bool)), key2
+    assert np.array_equal(got['reward'], ref['reward'])
+    assert ref['truncated'].sum() > 0
+
+
+def test_truncation_singletask_reward(gpu):
+    n = 64
+    env = ogbench_amd.make('pointmaze-medium-singletask-task2-v0', num_envs=n, device=gpu, max_episode_steps=4)
+    obs, info = env.reset(seed=3)
+    # singletask: fixed task 2, no goal noise
+    goal = info['goal'].cpu().numpy()
+    assert np.array_equal(goal, np.tile([[24.0, 0.0]], (n, 1)))
+    for t in range(4):
+        obs, rew, term, trunc, info = env.step(torch.zeros(n, 2))
+        assert (rew.cpu().numpy() == -1.0).all()
+        assert trunc.cpu().numpy().all() == (t == 3)
+
+
+def test_step_before_reset_and_bad_task(gpu):
+    env = _env(gpu, 4)
+    with pytest.raises(Exception, match='reset'):
+        env.step(torch.zeros(4, 2))
+    with pytest.raises(AssertionError, match='Task ID must be in'):
+        env.reset(options=dict(task_id=9))
+
+
+def test_teleport_moves_state_but_not_obs(gpu):
+    env = _env(gpu, 2, 'teleport')
+    env.reset(seed=1, options=dict(task_id=1, noise=torch.zeros(2, 4, dtype=torch.float64)))
+    sd = env.state_dict()
+    sd['qpos'] = torch.tensor([[20.0, 12.0], [5.0, 0.0]])  # first env on the in-portal (4,6)
+    env.load_state_dict(sd)
+    obs, *_ = env.step(torch.zeros(2, 2))
+    q = env.get_xy().cpu().numpy()
+    assert np.array_equal(obs.cpu().numpy()[0], [20.0, 12.0])
+    assert tuple(q[0]) in {(24.0, 0.0), (0.0, 20.0), (36.0, 20.0)}
+    assert np.array_equal(q[1], [5.0, 0.0])
