@@ -570,14 +570,14 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
 
 ogbx_status ogbx_maze_destroy(ogbx_maze_t e) {
   if (e == nullptr) return OGBX_OK;
-  hipSetDevice(e->device);
-  hipFree(e->S.qpos);
-  hipFree(e->S.goal);
-  hipFree(e->S.elapsed);
-  hipFree(e->S.task);
-  hipFree(e->S.episode);
-  hipFree(e->bfs);
-  hipFree(e->Pd);
+  (void)hipSetDevice(e->device);
+  (void)hipFree(e->S.qpos);
+  (void)hipFree(e->S.goal);
+  (void)hipFree(e->S.elapsed);
+  (void)hipFree(e->S.task);
+  (void)hipFree(e->S.episode);
+  (void)hipFree(e->bfs);
+  (void)hipFree(e->Pd);
   delete e;
   return OGBX_OK;
 }

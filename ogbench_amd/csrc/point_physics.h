@@ -100,63 +100,91 @@ __device__ inline void add_contact(const PointModel& pm, Contacts& c, int slot, 
   }
 }
 
-// Sphere vs. every wall box of the 3x3 neighbourhood (MuJoCo sphere-box
-// collision in the box frame; boxes are axis aligned, margin 0).  `wall` is the
-// map in LDS (row-major, 1 = wall).  Returns the number of contacts.
+// Exact sphere-box test of wall cell (i, j) (MuJoCo sphere-box collision in
+// the box frame; boxes are axis aligned, margin 0).  Appends to `c` on contact.
+__device__ inline void collide_box(const PointModel& pm, double x, double y, int i, int j,
+                                   Contacts& c, int& nc) {
+  const double hx = pm.box_hxy, hz = pm.box_hz;
+  const double px = x - (j * pm.unit - pm.off_x);
+  const double py = y - (i * pm.unit - pm.off_y);
+  const double pz = pm.sphere_z - pm.box_cz;
+  const double clx = px < -hx ? -hx : (px > hx ? hx : px);
+  const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+  const double clz = pz < -hz ? -hz : (pz > hz ? hz : pz);
+  const double tx = clx - px, ty = cly - py, tz = clz - pz;
+  const double d = sqrt(tx * tx + ty * ty + tz * tz);
+  if (d - pm.radius > 0.0 || nc >= kMaxContacts) return;
+  if (d > kMinVal) {
+    // centre outside the box: normal along (centre - closest point).
+    const double nx = -tx / d, ny = -ty / d;
+    add_contact(pm, c, nc, d - pm.radius, nx, ny, -ny, nx);
+  } else {
+    // centre inside the box: push out through the nearest face
+    // (faces ordered -x, +x, -y, +y, -z, +z; first strict minimum wins).
+    const double f0 = hx + px, f1 = hx - px, f2 = hx + py, f3 = hx - py, f4 = hz + pz,
+                 f5 = hz - pz;
+    int k = 0;
+    double best = f0;
+    if (f1 < best) { best = f1; k = 1; }
+    if (f2 < best) { best = f2; k = 2; }
+    if (f3 < best) { best = f3; k = 3; }
+    if (f4 < best) { best = f4; k = 4; }
+    if (f5 < best) { best = f5; k = 5; }
+    const double dist = -best - pm.radius;
+    const double sgn = (k & 1) ? 1.0 : -1.0;
+    if (k < 2) {
+      add_contact(pm, c, nc, dist, sgn, 0.0, 0.0, 1.0);
+    } else if (k < 4) {
+      add_contact(pm, c, nc, dist, 0.0, sgn, 1.0, 0.0);
+    } else {
+      // z face: Jn = 0, tangents e_x and e_y -> two pseudo-contacts.
+      add_contact(pm, c, nc, dist, 0.0, 0.0, 1.0, 0.0);
+      if (nc + 1 < kMaxContacts) add_contact(pm, c, ++nc, dist, 0.0, 0.0, 0.0, 1.0);
+    }
+  }
+  ++nc;
+}
+
+// All wall contacts of the sphere at (x, y).  Only boxes of the 3x3
+// neighbourhood can be touched (r < maze_unit/2); a neighbour on side s is a
+// candidate only if the centre is within r (+1e-9 slack) of that side of its
+// own cell, so the exact test above runs for <= 4 boxes instead of 9 and the
+// result equals the full scan.  `wall` is the map in LDS (row-major, 1 = wall).
 __device__ inline int collide_walls(const PointModel& pm, const uint8_t* wall, int H, int W,
                                     double x, double y, Contacts& c) {
 #pragma unroll
   for (int s = 0; s < kMaxContacts; ++s) {
     c.nx[s] = 0.0; c.ny[s] = 0.0; c.tx[s] = 0.0; c.ty[s] = 0.0; c.kp[s] = 0.0; c.w[s] = 0.0;
   }
-  const int i0 = (int)floor((y + pm.off_y + 0.5 * pm.unit) / pm.unit);
-  const int j0 = (int)floor((x + pm.off_x + 0.5 * pm.unit) / pm.unit);
-  const double dz = pm.sphere_z - pm.box_cz;
-  const double hx = pm.box_hxy, hz = pm.box_hz;
+  const double fi = floor((y + pm.off_y + 0.5 * pm.unit) / pm.unit);
+  const double fj = floor((x + pm.off_x + 0.5 * pm.unit) / pm.unit);
+  const int i0 = (int)fi, j0 = (int)fj;
+  const double lx = x - (fj * pm.unit - pm.off_x);  // offset from own cell centre
+  const double ly = y - (fi * pm.unit - pm.off_y);
+  const double reach = pm.box_hxy - pm.radius - 1e-9;
+  const int sx = lx >= reach ? 1 : (lx <= -reach ? -1 : 0);
+  const int sy = ly >= reach ? 1 : (ly <= -reach ? -1 : 0);
+  // candidate boxes packed 4 bits each: (di+1) | (dj+1) << 2; one exact test
+  // body in a rolled loop keeps the code (and the register file) small.
+  auto is_wall = [&](int i, int j) {
+    return i >= 0 && i < H && j >= 0 && j < W && wall[i * W + j] != 0;
+  };
+  uint32_t cand = 0, ncand = 0;
+  auto push = [&](int di, int dj) {
+    if (is_wall(i0 + di, j0 + dj)) {
+      cand |= (uint32_t)((di + 1) | ((dj + 1) << 2)) << (4 * ncand);
+      ++ncand;
+    }
+  };
+  push(0, 0);
+  if (sx != 0) push(0, sx);
+  if (sy != 0) push(sy, 0);
+  if (sx != 0 && sy != 0) push(sy, sx);
   int nc = 0;
 #pragma unroll 1
-  for (int nb = 0; nb < 9; ++nb) {
-    const int i = i0 + nb / 3 - 1, j = j0 + nb % 3 - 1;
-    const bool is_wall = i >= 0 && i < H && j >= 0 && j < W && wall[i * W + j];
-    if (!is_wall || nc >= kMaxContacts) continue;
-    const double px = x - (j * pm.unit - pm.off_x);
-    const double py = y - (i * pm.unit - pm.off_y);
-    const double pz = dz;
-    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
-    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
-    const double clz = pz < -hz ? -hz : (pz > hz ? hz : pz);
-    const double tx = clx - px, ty = cly - py, tz = clz - pz;
-    const double d = sqrt(tx * tx + ty * ty + tz * tz);
-    if (d - pm.radius > 0.0) continue;
-    if (d > kMinVal) {
-      // centre outside the box: normal along (centre - closest point).
-      const double nx = -tx / d, ny = -ty / d;
-      add_contact(pm, c, nc, d - pm.radius, nx, ny, -ny, nx);
-    } else {
-      // centre inside the box: push out through the nearest face
-      // (faces ordered -x, +x, -y, +y, -z, +z; first strict minimum wins).
-      const double f0 = hx + px, f1 = hx - px, f2 = hx + py, f3 = hx - py, f4 = hz + pz,
-                   f5 = hz - pz;
-      int k = 0;
-      double best = f0;
-      if (f1 < best) { best = f1; k = 1; }
-      if (f2 < best) { best = f2; k = 2; }
-      if (f3 < best) { best = f3; k = 3; }
-      if (f4 < best) { best = f4; k = 4; }
-      if (f5 < best) { best = f5; k = 5; }
-      const double dist = -best - pm.radius;
-      const double sgn = (k & 1) ? 1.0 : -1.0;
-      if (k < 2) {
-        add_contact(pm, c, nc, dist, sgn, 0.0, 0.0, 1.0);
-      } else if (k < 4) {
-        add_contact(pm, c, nc, dist, 0.0, sgn, 1.0, 0.0);
-      } else {
-        // z face: Jn = 0, tangents e_x and e_y -> two pseudo-contacts.
-        add_contact(pm, c, nc, dist, 0.0, 0.0, 1.0, 0.0);
-        if (nc + 1 < kMaxContacts) add_contact(pm, c, ++nc, dist, 0.0, 0.0, 0.0, 1.0);
-      }
-    }
-    ++nc;
+  for (uint32_t k = 0; k < ncand; ++k) {
+    const uint32_t code = (cand >> (4 * k)) & 15u;
+    collide_box(pm, x, y, i0 + (int)(code & 3u) - 1, j0 + (int)(code >> 2) - 1, c, nc);
   }
   c.n = nc;
   return nc;
@@ -168,8 +196,8 @@ __device__ inline int collide_walls(const PointModel& pm, const uint8_t* wall, i
 // qacc for the given contacts at velocity (vx, vy).  See the header comment for
 // the u = a + B v formulation.  Loops run to the compile-time bound with an
 // `s < n` guard so nothing is dynamically indexed (no scratch).
-__device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
-                                 double* ax_out, double* ay_out) {
+__device__ inline void solve_acc_newton(const PointModel& pm, const Contacts& c, double vx,
+                                        double vy, double* ax_out, double* ay_out) {
   const double m = pm.mass, Df = pm.D_floor;
   const double mf = m + Df;
   const double bvx = pm.B * vx, bvy = pm.B * vy;
@@ -287,6 +315,81 @@ __device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double
   }
   *ax_out = ux - bvx;
   *ay_out = uy - bvy;
+}
+
+// Exact minimiser for exactly ONE wall contact, by active-set enumeration in
+// the contact frame (un = n.u, ut = t.u).  With M = m + Df, cu = m B v / M the
+// floor-only minimiser, e = kp and residuals r+ = un+e+ut, r- = un+e-ut,
+// r0 = un+e, the consistent active sets are {}, {+}, {-}, {0,+}, {0,-},
+// {0,+,-} ({0} alone and {+,-} without 0 are infeasible); each is a closed-
+// form 2x2 solve and exactly one is consistent.  Returns false if rounding
+// leaves none consistent (the caller then runs the Newton solver).
+__device__ inline bool solve_one_contact(const PointModel& pm, const Contacts& c, double cux,
+                                         double cuy, double* ux, double* uy) {
+  const double M = pm.mass + pm.D_floor;
+  const double nx = c.nx[0], ny = c.ny[0], tx = c.tx[0], ty = c.ty[0];
+  const double e = c.kp[0], w = c.w[0];
+  const double cn = nx * cux + ny * cuy, ct = tx * cux + ty * cuy;
+  double un, ut;
+  bool ok = true;
+  // {}: u = cu
+  if (cn + e + ct >= 0.0 && cn + e - ct >= 0.0) {
+    un = cn;
+    ut = ct;
+  } else {
+    const double i2 = 1.0 / (M + 2.0 * w);
+    // {+}: rank-1 update along J = n + t (|J|^2 = 2)
+    const double rp = cn + e + ct;
+    const double bpn = cn - w * rp * i2, bpt = ct - w * rp * i2;
+    // {-}: J = n - t
+    const double rm = cn + e - ct;
+    const double bmn = cn - w * rm * i2, bmt = ct + w * rm * i2;
+    // {0,+} / {0,-}: [[M+3w, +-w], [+-w, M+w]] u = [M cn - 3 w e, M ct -+ w e]
+    const double a11 = M + 3.0 * w, a22 = M + w;
+    const double idet = 1.0 / (a11 * a22 - w * w);
+    const double r1 = M * cn - 3.0 * w * e;
+    const double dpn = (a22 * r1 - w * (M * ct - w * e)) * idet;
+    const double dpt = (a11 * (M * ct - w * e) - w * r1) * idet;
+    const double dmn = (a22 * r1 + w * (M * ct + w * e)) * idet;
+    const double dmt = (a11 * (M * ct + w * e) + w * r1) * idet;
+    // {0,+,-}: decoupled
+    const double fn = (M * cn - 4.0 * w * e) / (M + 4.0 * w);
+    const double ft = M * ct * i2;
+    if (bpn + e + bpt < 0.0 && bpn + e - bpt >= 0.0 && bpn + e >= 0.0) {
+      un = bpn; ut = bpt;
+    } else if (bmn + e - bmt < 0.0 && bmn + e + bmt >= 0.0 && bmn + e >= 0.0) {
+      un = bmn; ut = bmt;
+    } else if (dpn + e < 0.0 && dpn + e + dpt < 0.0 && dpn + e - dpt >= 0.0) {
+      un = dpn; ut = dpt;
+    } else if (dmn + e < 0.0 && dmn + e - dmt < 0.0 && dmn + e + dmt >= 0.0) {
+      un = dmn; ut = dmt;
+    } else if (fn + e + ft < 0.0 && fn + e - ft < 0.0) {
+      un = fn; ut = ft;
+    } else {
+      ok = false;
+      un = cn;
+      ut = ct;
+    }
+  }
+  *ux = un * nx + ut * tx;
+  *uy = un * ny + ut * ty;
+  return ok;
+}
+
+__device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
+                                 double* ax_out, double* ay_out) {
+  if (c.n == 1) {
+    const double mf = pm.mass + pm.D_floor;
+    const double bvx = pm.B * vx, bvy = pm.B * vy;
+    const double cux = (pm.mass * bvx) / mf, cuy = (pm.mass * bvy) / mf;
+    double ux, uy;
+    if (solve_one_contact(pm, c, cux, cuy, &ux, &uy)) {
+      *ax_out = ux - bvx;
+      *ay_out = uy - bvy;
+      return;
+    }
+  }
+  solve_acc_newton(pm, c, vx, vy, ax_out, ay_out);
 }
 
 // One PointEnv step starting from qpos + delta with qvel = 0.  Returns 1 if a
