@@ -425,7 +425,9 @@ static PointModel make_point_model(double unit, double off) {
   pm.imp_dmax = 0.95;
   pm.imp_width = 0.001;
   pm.imp_mid = 0.5;
-  pm.imp_power = 2.0;
+  const double power = 2.0;
+  pm.imp_a = 1.0 / std::pow(pm.imp_mid, power - 1.0);
+  pm.imp_b = 1.0 / std::pow(1.0 - pm.imp_mid, power - 1.0);
   const double dmax = pm.imp_dmax;
   pm.K = 1.0 / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
   pm.B = 2.0 / (dmax * timeconst);
@@ -440,13 +442,26 @@ static PointModel make_point_model(double unit, double off) {
   // each pair is active, which sums to 1/2 Df |a + B v|^2.
   pm.D_floor = 1.0 / Rf;
   pm.radius = r;
+  pm.r2_hi = r * r * (1.0 + 1e-12);
   pm.sphere_z = 0.7;
   pm.box_cz = 0.5 / 2.0 * unit;  // maze_height/2 * maze_unit (maze.py:233)
   pm.box_hz = 0.5 / 2.0 * unit;
   pm.box_hxy = unit / 2.0;
   pm.unit = unit;
+  pm.inv_unit = 1.0 / unit;  // exact for unit = 4
   pm.off_x = off;
   pm.off_y = off;
+  // solver constants
+  pm.M = pm.mass + pm.D_floor;
+  pm.m_over_M = pm.mass / pm.M;
+  double Rmax = (1.0 - dmax) * pm.diag / dmax;
+  if (Rmax < kMinVal) Rmax = kMinVal;
+  pm.w_max = 1.0 / Rmax;
+  pm.kp_max = pm.K * dmax;
+  const double w = pm.w_max, M = pm.M;
+  pm.inv_M2w = 1.0 / (M + 2.0 * w);
+  pm.inv_M4w = 1.0 / (M + 4.0 * w);
+  pm.inv_det3 = 1.0 / ((M + 3.0 * w) * (M + w) - w * w);
   return pm;
 }
 

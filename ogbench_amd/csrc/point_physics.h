@@ -12,8 +12,10 @@
 //     condim 3, pyramidal cone, mu = 1 -> edges J = Jn +- mu*Jt_k.
 //   * Soft constraint per edge: aref = -B*(J.v) - K*imp*dist, cost 1/2*D*r^2 on
 //     r = J.a - aref < 0, D = 1/R, R = max(mjMINVAL, (1-imp)/imp*diagApprox).
-//   * qacc = argmin 1/2 m|a|^2 + sum_edges cost; solved exactly (Newton with an
-//     exact piecewise-quadratic line search, stopping on a consistent piece).
+//   * qacc = argmin 1/2 m|a|^2 + sum_edges cost, solved exactly: closed-form
+//     active-set enumeration for one wall contact, full-step semismooth Newton
+//     (stops when the active set reproduces itself) for several, and a damped
+//     Newton with Armijo backtracking as the safety net.
 //   * RK4 tableau of mj_RungeKutta; mj_advance uses the B-weighted velocity.
 //
 // Because every edge has aref = -B*J.v - kp with the same B, the residual of an
@@ -38,12 +40,20 @@ struct PointModel {
   double B, K;        // solref-derived damping / stiffness
   double diag;        // diagApprox of one pyramid edge
   double D_floor;     // 1/R at imp(dist = 0) = solimp[0]
-  double imp_dmin, imp_dmax, imp_width, imp_mid, imp_power;
+  double imp_dmin, imp_dmax, imp_width;
+  double imp_mid, imp_a, imp_b;  // power-2 sigmoid: y = a x^2 | 1 - b (1-x)^2
   double radius;      // sphere radius 0.7
+  double r2_hi;       // radius^2 * (1 + 1e-12): sqrt-free rejection bound
   double sphere_z;    // sphere centre height 0.7
   double box_cz, box_hz;  // wall box centre z / half height
   double box_hxy;     // wall box half size in x and y (maze_unit/2)
-  double unit, off_x, off_y;
+  double unit, inv_unit, off_x, off_y;
+  // derived solver constants (host-computed, see make_point_model)
+  double M;           // m + D_floor
+  double m_over_M;    // m / M
+  double w_max;       // D of an edge at imp = dmax (|dist| >= width)
+  double kp_max;      // K * dmax
+  double inv_M2w, inv_M4w, inv_det3;  // closed-form reciprocals at w = w_max
   int32_t nsub;       // frame_skip (5)
   int32_t pad_;
 };
@@ -61,32 +71,29 @@ struct Contacts {
   double w[kMaxContacts];                     // D = 1/R of one edge
 };
 
-// MuJoCo getimpedance(): sigmoid between dmin and dmax over |dist|/width.
-__device__ inline double impedance(const PointModel& pm, double dist) {
-  double x = dist / pm.imp_width;
-  if (x < 0) x = -x;
-  if (x >= 1.0) return pm.imp_dmax;
-  if (x <= 0.0) return pm.imp_dmin;
-  double y;
-  if (x <= pm.imp_mid) {
-    double a = 1.0 / pow(pm.imp_mid, pm.imp_power - 1.0);
-    y = a * pow(x, pm.imp_power);
-  } else {
-    double b = 1.0 / pow(1.0 - pm.imp_mid, pm.imp_power - 1.0);
-    y = 1.0 - b * pow(1.0 - x, pm.imp_power);
-  }
-  return pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
-}
-
 // Store one contact into slot `slot` (static predicated writes keep Contacts
-// in VGPRs).
+// in VGPRs).  imp = MuJoCo getimpedance() with solimp power 2; beyond the
+// transition width it is dmax and D, K*imp are the precomputed constants.
 __device__ inline void add_contact(const PointModel& pm, Contacts& c, int slot, double dist,
                                    double nx, double ny, double tx, double ty) {
-  double imp = impedance(pm, dist);
-  double R = (1.0 - imp) * pm.diag / imp;
-  if (R < kMinVal) R = kMinVal;
-  double D = 1.0 / R;
-  double kp = pm.K * imp * dist;
+  double D, kp;
+  const double x = fabs(dist / pm.imp_width);
+  if (x >= 1.0) {
+    D = pm.w_max;
+    kp = pm.kp_max * dist;
+  } else {
+    double imp;
+    if (x <= 0.0) {
+      imp = pm.imp_dmin;
+    } else {
+      const double y = x <= pm.imp_mid ? pm.imp_a * (x * x) : 1.0 - pm.imp_b * ((1.0 - x) * (1.0 - x));
+      imp = pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
+    }
+    double R = (1.0 - imp) * pm.diag / imp;
+    if (R < kMinVal) R = kMinVal;
+    D = 1.0 / R;
+    kp = pm.K * imp * dist;
+  }
 #pragma unroll
   for (int s = 0; s < kMaxContacts; ++s) {
     if (s == slot) {
@@ -112,11 +119,14 @@ __device__ inline void collide_box(const PointModel& pm, double x, double y, int
   const double cly = py < -hx ? -hx : (py > hx ? hx : py);
   const double clz = pz < -hz ? -hz : (pz > hz ? hz : pz);
   const double tx = clx - px, ty = cly - py, tz = clz - pz;
-  const double d = sqrt(tx * tx + ty * ty + tz * tz);
-  if (d - pm.radius > 0.0 || nc >= kMaxContacts) return;
+  const double d2 = tx * tx + ty * ty + tz * tz;
+  if (d2 > pm.r2_hi || nc >= kMaxContacts) return;  // certainly d - r > 0
+  const double d = sqrt(d2);
+  if (d - pm.radius > 0.0) return;
   if (d > kMinVal) {
     // centre outside the box: normal along (centre - closest point).
-    const double nx = -tx / d, ny = -ty / d;
+    const double inv = 1.0 / d;
+    const double nx = -tx * inv, ny = -ty * inv;
     add_contact(pm, c, nc, d - pm.radius, nx, ny, -ny, nx);
   } else {
     // centre inside the box: push out through the nearest face
@@ -148,16 +158,16 @@ __device__ inline void collide_box(const PointModel& pm, double x, double y, int
 // All wall contacts of the sphere at (x, y).  Only boxes of the 3x3
 // neighbourhood can be touched (r < maze_unit/2); a neighbour on side s is a
 // candidate only if the centre is within r (+1e-9 slack) of that side of its
-// own cell, so the exact test above runs for <= 4 boxes instead of 9 and the
-// result equals the full scan.  `wall` is the map in LDS (row-major, 1 = wall).
+// own cell, so the exact test runs for <= 4 boxes instead of 9 and the result
+// equals the full scan.  `wall` is the map in LDS (row-major, 1 = wall).
 __device__ inline int collide_walls(const PointModel& pm, const uint8_t* wall, int H, int W,
                                     double x, double y, Contacts& c) {
 #pragma unroll
   for (int s = 0; s < kMaxContacts; ++s) {
     c.nx[s] = 0.0; c.ny[s] = 0.0; c.tx[s] = 0.0; c.ty[s] = 0.0; c.kp[s] = 0.0; c.w[s] = 0.0;
   }
-  const double fi = floor((y + pm.off_y + 0.5 * pm.unit) / pm.unit);
-  const double fj = floor((x + pm.off_x + 0.5 * pm.unit) / pm.unit);
+  const double fi = floor((y + pm.off_y + 0.5 * pm.unit) * pm.inv_unit);
+  const double fj = floor((x + pm.off_x + 0.5 * pm.unit) * pm.inv_unit);
   const int i0 = (int)fi, j0 = (int)fj;
   const double lx = x - (fj * pm.unit - pm.off_x);  // offset from own cell centre
   const double ly = y - (fi * pm.unit - pm.off_y);
@@ -190,154 +200,37 @@ __device__ inline int collide_walls(const PointModel& pm, const uint8_t* wall, i
   return nc;
 }
 
-// Edge e of contact s at u, with a = n.u + kp and b = t.u:
+// ---------------------------------------------------------------------------
+// Solvers, all in u = a + B v (see the header comment):
+//   f(u) = 1/2 M |u - cu|^2 + sum_s sum_e 1/2 w_se min(0, r_se)^2,
+//   M = m + Df, cu = m B v / M, and for contact s with a = n.u + kp, b = t.u:
 //   e0: r = a + b (weight w), e1: r = a - b (w), e2: r = a (2w).
 
-// qacc for the given contacts at velocity (vx, vy).  See the header comment for
-// the u = a + B v formulation.  Loops run to the compile-time bound with an
-// `s < n` guard so nothing is dynamically indexed (no scratch).
-__device__ inline void solve_acc_newton(const PointModel& pm, const Contacts& c, double vx,
-                                        double vy, double* ax_out, double* ay_out) {
-  const double m = pm.mass, Df = pm.D_floor;
-  const double mf = m + Df;
-  const double bvx = pm.B * vx, bvy = pm.B * vy;
-  const int n = c.n;
-  // floor-only minimiser: u = m B v / (m + Df)
-  double ux = (m * bvx) / mf;
-  double uy = (m * bvy) / mf;
-  if (n > 0) {
-    for (int it = 0; it < 24; ++it) {
-      // gradient / Hessian of the current piece
-      const double gfx = m * (ux - bvx) + Df * ux;
-      const double gfy = m * (uy - bvy) + Df * uy;
-      double gx = gfx, gy = gfy, h00 = mf, h01 = 0.0, h11 = mf;
-      uint32_t act = 0;
-#pragma unroll
-      for (int s = 0; s < kMaxContacts; ++s) {
-        if (s < n) {
-          const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
-          const double b = c.tx[s] * ux + c.ty[s] * uy;
-          const double w = c.w[s];
-#pragma unroll
-          for (int e = 0; e < 3; ++e) {
-            const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
-            const double we = e == 2 ? 2.0 * w : w;
-            const double r = e == 2 ? a : a + sg * b;
-            if (r < 0.0) {
-              const double jx = e == 2 ? c.nx[s] : c.nx[s] + sg * c.tx[s];
-              const double jy = e == 2 ? c.ny[s] : c.ny[s] + sg * c.ty[s];
-              act |= 1u << (3 * s + e);
-              gx += we * r * jx;
-              gy += we * r * jy;
-              h00 += we * jx * jx;
-              h01 += we * jx * jy;
-              h11 += we * jy * jy;
-            }
-          }
-        }
-      }
-      if (gx == 0.0 && gy == 0.0) break;
-      const double det = h00 * h11 - h01 * h01;
-      const double px = -(h11 * gx - h01 * gy) / det;
-      const double py = -(h00 * gy - h01 * gx) / det;
-
-      // exact line search on phi(alpha) = f(u + alpha p): walk the edge
-      // breakpoints in increasing alpha until phi' changes sign.
-      double brk[3 * kMaxContacts];
-      uint32_t flag = 0, cross = 0;
-#pragma unroll
-      for (int s = 0; s < kMaxContacts; ++s) {
-        const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
-        const double b = c.tx[s] * ux + c.ty[s] * uy;
-        const double qa = c.nx[s] * px + c.ny[s] * py;
-        const double qb = c.tx[s] * px + c.ty[s] * py;
-#pragma unroll
-        for (int e = 0; e < 3; ++e) {
-          const int k = 3 * s + e;
-          const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
-          const double r = e == 2 ? a : a + sg * b;
-          const double q = e == 2 ? qa : qa + sg * qb;
-          brk[k] = INFINITY;
-          if (s < n) {
-            if (r < 0.0 || (r == 0.0 && q < 0.0)) flag |= 1u << k;
-            if ((r < 0.0 && q > 0.0) || (r > 0.0 && q < 0.0)) {
-              brk[k] = -r / q;
-              cross |= 1u << k;
-            }
-          }
-        }
-      }
-      const uint32_t flag0 = flag;
-      const double base0 = px * gfx + py * gfy;
-      const double base1 = mf * (px * px + py * py);
-      double alpha = 0.0;
-      bool crossed = false;
-      for (int seg = 0; seg <= 3 * kMaxContacts; ++seg) {
-        double c0 = base0, c1 = base1, beta = INFINITY;
-#pragma unroll
-        for (int s = 0; s < kMaxContacts; ++s) {
-          const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
-          const double b = c.tx[s] * ux + c.ty[s] * uy;
-          const double qa = c.nx[s] * px + c.ny[s] * py;
-          const double qb = c.tx[s] * px + c.ty[s] * py;
-#pragma unroll
-          for (int e = 0; e < 3; ++e) {
-            const int k = 3 * s + e;
-            if (flag & (1u << k)) {
-              const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
-              const double we = e == 2 ? 2.0 * c.w[s] : c.w[s];
-              const double r = e == 2 ? a : a + sg * b;
-              const double q = e == 2 ? qa : qa + sg * qb;
-              c0 += we * q * r;
-              c1 += we * q * q;
-            }
-            if ((cross & (1u << k)) && brk[k] < beta) beta = brk[k];
-          }
-        }
-        const double ac = -c0 / c1;
-        if (ac <= beta) {
-          alpha = ac;
-          break;
-        }
-        alpha = beta;
-        crossed = true;
-#pragma unroll
-        for (int k = 0; k < 3 * kMaxContacts; ++k)
-          if ((cross & (1u << k)) && brk[k] == beta) {
-            flag ^= 1u << k;
-            cross &= ~(1u << k);
-          }
-      }
-      ux += alpha * px;
-      uy += alpha * py;
-      if (!crossed && flag0 == act) break;  // exact minimiser of a consistent piece
-    }
-  }
-  *ax_out = ux - bvx;
-  *ay_out = uy - bvy;
-}
-
 // Exact minimiser for exactly ONE wall contact, by active-set enumeration in
-// the contact frame (un = n.u, ut = t.u).  With M = m + Df, cu = m B v / M the
-// floor-only minimiser, e = kp and residuals r+ = un+e+ut, r- = un+e-ut,
-// r0 = un+e, the consistent active sets are {}, {+}, {-}, {0,+}, {0,-},
-// {0,+,-} ({0} alone and {+,-} without 0 are infeasible); each is a closed-
-// form 2x2 solve and exactly one is consistent.  Returns false if rounding
-// leaves none consistent (the caller then runs the Newton solver).
+// the contact frame (un = n.u, ut = t.u).  The consistent active sets are {},
+// {+}, {-}, {0,+}, {0,-}, {0,+,-} ({0} alone and {+,-} without 0 are
+// infeasible); each is a closed-form 2x2 solve and exactly one is consistent.
+// Returns false if rounding leaves none consistent (caller falls back).
 __device__ inline bool solve_one_contact(const PointModel& pm, const Contacts& c, double cux,
                                          double cuy, double* ux, double* uy) {
-  const double M = pm.mass + pm.D_floor;
+  const double M = pm.M;
   const double nx = c.nx[0], ny = c.ny[0], tx = c.tx[0], ty = c.ty[0];
   const double e = c.kp[0], w = c.w[0];
   const double cn = nx * cux + ny * cuy, ct = tx * cux + ty * cuy;
-  double un, ut;
+  double un = cn, ut = ct;
   bool ok = true;
-  // {}: u = cu
-  if (cn + e + ct >= 0.0 && cn + e - ct >= 0.0) {
-    un = cn;
-    ut = ct;
-  } else {
-    const double i2 = 1.0 / (M + 2.0 * w);
+  if (!(cn + e + ct >= 0.0 && cn + e - ct >= 0.0)) {  // {} is not consistent
+    double i2, i4, idet;
+    const double a11 = M + 3.0 * w, a22 = M + w;
+    if (w == pm.w_max) {
+      i2 = pm.inv_M2w;
+      i4 = pm.inv_M4w;
+      idet = pm.inv_det3;
+    } else {
+      i2 = 1.0 / (M + 2.0 * w);
+      i4 = 1.0 / (M + 4.0 * w);
+      idet = 1.0 / (a11 * a22 - w * w);
+    }
     // {+}: rank-1 update along J = n + t (|J|^2 = 2)
     const double rp = cn + e + ct;
     const double bpn = cn - w * rp * i2, bpt = ct - w * rp * i2;
@@ -345,16 +238,12 @@ __device__ inline bool solve_one_contact(const PointModel& pm, const Contacts& c
     const double rm = cn + e - ct;
     const double bmn = cn - w * rm * i2, bmt = ct + w * rm * i2;
     // {0,+} / {0,-}: [[M+3w, +-w], [+-w, M+w]] u = [M cn - 3 w e, M ct -+ w e]
-    const double a11 = M + 3.0 * w, a22 = M + w;
-    const double idet = 1.0 / (a11 * a22 - w * w);
     const double r1 = M * cn - 3.0 * w * e;
-    const double dpn = (a22 * r1 - w * (M * ct - w * e)) * idet;
-    const double dpt = (a11 * (M * ct - w * e) - w * r1) * idet;
-    const double dmn = (a22 * r1 + w * (M * ct + w * e)) * idet;
-    const double dmt = (a11 * (M * ct + w * e) + w * r1) * idet;
+    const double rp2 = M * ct - w * e, rm2 = M * ct + w * e;
+    const double dpn = (a22 * r1 - w * rp2) * idet, dpt = (a11 * rp2 - w * r1) * idet;
+    const double dmn = (a22 * r1 + w * rm2) * idet, dmt = (a11 * rm2 + w * r1) * idet;
     // {0,+,-}: decoupled
-    const double fn = (M * cn - 4.0 * w * e) / (M + 4.0 * w);
-    const double ft = M * ct * i2;
+    const double fn = (M * cn - 4.0 * w * e) * i4, ft = M * ct * i2;
     if (bpn + e + bpt < 0.0 && bpn + e - bpt >= 0.0 && bpn + e >= 0.0) {
       un = bpn; ut = bpt;
     } else if (bmn + e - bmt < 0.0 && bmn + e + bmt >= 0.0 && bmn + e >= 0.0) {
@@ -367,8 +256,6 @@ __device__ inline bool solve_one_contact(const PointModel& pm, const Contacts& c
       un = fn; ut = ft;
     } else {
       ok = false;
-      un = cn;
-      ut = ct;
     }
   }
   *ux = un * nx + ut * tx;
@@ -376,20 +263,102 @@ __device__ inline bool solve_one_contact(const PointModel& pm, const Contacts& c
   return ok;
 }
 
-__device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
-                                 double* ax_out, double* ay_out) {
-  if (c.n == 1) {
-    const double mf = pm.mass + pm.D_floor;
-    const double bvx = pm.B * vx, bvy = pm.B * vy;
-    const double cux = (pm.mass * bvx) / mf, cuy = (pm.mass * bvy) / mf;
-    double ux, uy;
-    if (solve_one_contact(pm, c, cux, cuy, &ux, &uy)) {
-      *ax_out = ux - bvx;
-      *ay_out = uy - bvy;
-      return;
+// Residuals, gradient and Hessian of f at u.  Returns the active-edge mask.
+__device__ inline uint32_t eval_piece(const PointModel& pm, const Contacts& c, double cux,
+                                      double cuy, double ux, double uy, double* g, double* h,
+                                      double* fval) {
+  const double M = pm.M;
+  g[0] = M * (ux - cux);
+  g[1] = M * (uy - cuy);
+  h[0] = M; h[1] = 0.0; h[2] = M;
+  double f = 0.5 * M * ((ux - cux) * (ux - cux) + (uy - cuy) * (uy - cuy));
+  uint32_t act = 0;
+#pragma unroll
+  for (int s = 0; s < kMaxContacts; ++s) {
+    if (s < c.n) {
+      const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
+      const double b = c.tx[s] * ux + c.ty[s] * uy;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
+        const double r = e == 2 ? a : a + sg * b;
+        if (r < 0.0) {
+          const double we = e == 2 ? 2.0 * c.w[s] : c.w[s];
+          const double jx = e == 2 ? c.nx[s] : c.nx[s] + sg * c.tx[s];
+          const double jy = e == 2 ? c.ny[s] : c.ny[s] + sg * c.ty[s];
+          act |= 1u << (3 * s + e);
+          g[0] += we * r * jx;
+          g[1] += we * r * jy;
+          h[0] += we * jx * jx;
+          h[1] += we * jx * jy;
+          h[2] += we * jy * jy;
+          f += 0.5 * we * r * r;
+        }
+      }
     }
   }
-  solve_acc_newton(pm, c, vx, vy, ax_out, ay_out);
+  *fval = f;
+  return act;
+}
+
+// Several contacts: full-step semismooth Newton; u is optimal once the active
+// set at the Newton point equals the set the step was computed on.  Safety
+// net: damped Newton with Armijo backtracking (monotone, globally convergent).
+__device__ inline void solve_newton(const PointModel& pm, const Contacts& c, double cux,
+                                    double cuy, double* ux_io, double* uy_io) {
+  double ux = *ux_io, uy = *uy_io;
+  double g[2], h[3], f;
+  uint32_t prev = 0xFFFFFFFFu;
+  bool done = false;
+#pragma unroll 1
+  for (int it = 0; it < 8; ++it) {
+    const uint32_t act = eval_piece(pm, c, cux, cuy, ux, uy, g, h, &f);
+    if (act == prev || (g[0] == 0.0 && g[1] == 0.0)) {
+      done = true;
+      break;
+    }
+    const double idet = 1.0 / (h[0] * h[2] - h[1] * h[1]);
+    ux -= (h[2] * g[0] - h[1] * g[1]) * idet;
+    uy -= (h[0] * g[1] - h[1] * g[0]) * idet;
+    prev = act;
+  }
+  if (!done) {
+    ux = cux;
+    uy = cuy;
+#pragma unroll 1
+    for (int it = 0; it < 64; ++it) {
+      eval_piece(pm, c, cux, cuy, ux, uy, g, h, &f);
+      const double idet = 1.0 / (h[0] * h[2] - h[1] * h[1]);
+      const double px = -(h[2] * g[0] - h[1] * g[1]) * idet;
+      const double py = -(h[0] * g[1] - h[1] * g[0]) * idet;
+      if (fabs(px) + fabs(py) <= 1e-16 * (1.0 + fabs(ux) + fabs(uy))) break;
+      const double slope = g[0] * px + g[1] * py;
+      double t = 1.0, g2[2], h2[3], f2;
+#pragma unroll 1
+      for (int bt = 0; bt < 60; ++bt) {
+        eval_piece(pm, c, cux, cuy, ux + t * px, uy + t * py, g2, h2, &f2);
+        if (f2 <= f + 1e-6 * t * slope) break;
+        t *= 0.5;
+      }
+      ux += t * px;
+      uy += t * py;
+    }
+  }
+  *ux_io = ux;
+  *uy_io = uy;
+}
+
+// qacc of the point mass at velocity (vx, vy) for the given wall contacts.
+__device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
+                                 double* ax_out, double* ay_out) {
+  const double bvx = pm.B * vx, bvy = pm.B * vy;
+  const double cux = pm.m_over_M * bvx, cuy = pm.m_over_M * bvy;  // floor-only minimiser
+  double ux = cux, uy = cuy;
+  bool solved = c.n == 0;
+  if (c.n == 1) solved = solve_one_contact(pm, c, cux, cuy, &ux, &uy);
+  if (!solved) solve_newton(pm, c, cux, cuy, &ux, &uy);
+  *ax_out = ux - bvx;
+  *ay_out = uy - bvy;
 }
 
 // One PointEnv step starting from qpos + delta with qvel = 0.  Returns 1 if a

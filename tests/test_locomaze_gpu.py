@@ -47,7 +47,7 @@ def test_physics_matches_oracle_with_contacts(gpu, maze, f64):
     ref, rc = orc.physics(maze, q, a, nthreads=8)
     got = out.cpu().numpy()
     assert np.array_equal(contact.cpu().numpy(), rc)
-    assert rc.mean() > 0.2  # the test really exercises contacts
+    assert rc.mean() > (0.05 if maze == "arena" else 0.2)  # the test really exercises contacts
     assert np.abs(got - ref).max() <= TOL
     assert np.array_equal(got[rc == 0], ref[rc == 0])
 
