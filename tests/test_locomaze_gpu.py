@@ -132,7 +132,7 @@ def test_truncation_singletask_reward(gpu):
     obs, info = env.reset(seed=3)
     # singletask: fixed task 2, no goal noise
     goal = info['goal'].cpu().numpy()
-    assert np.array_equal(goal, np.tile([[24.0, 0.0]], (n, 1)))
+    assert np.array_equal(goal, np.tile([[20.0, 0.0]], (n, 1)))  # task2 goal (1,6)
     for t in range(4):
         obs, rew, term, trunc, info = env.step(torch.zeros(n, 2))
         assert (rew.cpu().numpy() == -1.0).all()
