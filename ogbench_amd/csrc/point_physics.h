@@ -59,9 +59,11 @@ struct PointModel {
 };
 
 constexpr double kMinVal = 1e-15;  // mjMINVAL
-// A sphere in an empty cell touches at most 3 wall boxes; the 4th slot holds
-// the second pseudo-contact of a (pathological) contact through a box z face.
-constexpr int kMaxContacts = 4;
+// A sphere whose centre lies in an empty cell touches at most 3 wall boxes
+// (two faces + the corner box between them).  States with the centre deep in
+// a wall (contact through a box z face = two pseudo-contacts) are unreachable
+// from any reset; there, contacts beyond 3 are dropped.
+constexpr int kMaxContacts = 3;
 
 struct Contacts {
   int n;
@@ -121,12 +123,26 @@ __device__ inline void collide_box(const PointModel& pm, double x, double y, int
   const double tx = clx - px, ty = cly - py, tz = clz - pz;
   const double d2 = tx * tx + ty * ty + tz * tz;
   if (d2 > pm.r2_hi || nc >= kMaxContacts) return;  // certainly d - r > 0
-  const double d = sqrt(d2);
+  // Face contacts (one of tx, ty zero; tz is 0 for every wall) need neither
+  // sqrt nor division: sqrt(fl(t*t)) == |t| and -t/|t| == -sign(t) exactly.
+  double d, nx, ny;
+  if (ty == 0.0 && tz == 0.0) {
+    d = fabs(tx);
+    nx = tx > 0.0 ? -1.0 : 1.0;
+    ny = -0.0 * ty;
+  } else if (tx == 0.0 && tz == 0.0) {
+    d = fabs(ty);
+    nx = -0.0 * tx;
+    ny = ty > 0.0 ? -1.0 : 1.0;
+  } else {
+    d = sqrt(d2);
+    const double inv = 1.0 / d;
+    nx = -tx * inv;
+    ny = -ty * inv;
+  }
   if (d - pm.radius > 0.0) return;
   if (d > kMinVal) {
     // centre outside the box: normal along (centre - closest point).
-    const double inv = 1.0 / d;
-    const double nx = -tx * inv, ny = -ty * inv;
     add_contact(pm, c, nc, d - pm.radius, nx, ny, -ny, nx);
   } else {
     // centre inside the box: push out through the nearest face
