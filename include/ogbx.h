@@ -158,6 +158,108 @@ ogbx_status ogbx_maze_oracle_subgoal(ogbx_maze_t env, const double* start_xy,
                                      const double* goal_xy, int64_t n, double* subgoal_xy,
                                      void* stream);
 
+
+/* ======================================================================
+ * Offline replay: fused index-gather + hindsight goal relabel
+ * (impls/utils/datasets.py: Dataset.get_random_idxs/get_subset :65-83,
+ *  GCDataset.sample :213-294, GCDataset.sample_goals :296-327)
+ * ====================================================================== */
+
+/* One dataset column to gather into the batch. */
+typedef struct {
+  const void* src;   /* device, [num_rows, row_bytes] contiguous */
+  void* dst;         /* device, [num_batches * batch, row_bytes] */
+  int64_t row_bytes; /* bytes of one row (multiple of 4 uses dword copies) */
+  int32_t select;    /* 0 = idxs, 1 = min(idxs+1, R-1) (next_observations,
+                        datasets.py:82), 2 = value goal, 3 = actor goal */
+  int32_t pad_;
+} ogbx_gc_column;
+
+/* Static description of an HBM-resident trajectory buffer. */
+typedef struct {
+  int64_t num_rows;          /* R = Dataset.size (datasets.py:56)                */
+  const int64_t* valid_idxs; /* device [num_valid] = nonzero(valids > 0) or NULL */
+  int64_t num_valid;         /* (NULL -> randint(R), datasets.py:65-70)          */
+  const int64_t* traj_end;   /* device [R]: terminal_locs[searchsorted(
+                                terminal_locs, row)] (datasets.py:309)           */
+} ogbx_gc_buffer;
+
+/* Goal-sampling configuration (GCDataset config keys, datasets.py:155-170).
+ * *_traj_thresh = p_trajgoal / (1 - p_curgoal) computed by the caller in
+ * float64 exactly as datasets.py:321.  *_cur_is_one = (p_curgoal == 1.0). */
+typedef struct {
+  double value_p_curgoal, value_traj_thresh, value_discount;
+  double actor_p_curgoal, actor_traj_thresh, actor_discount;
+  int32_t value_geom_sample, actor_geom_sample;
+  int32_t value_cur_is_one, actor_cur_is_one;
+  int32_t gc_negative;
+  int32_t pad_;
+} ogbx_gc_config;
+
+/* Injected draws (parity mode).  Each pointer is device [num_batches*batch]
+ * or NULL; a NULL pointer means "draw it from Philox".  The values are the
+ * raw outputs of the reference's np.random calls in call order (datasets.py:
+ * 67, 305, 312 or 316, 321, 325):
+ *   pick      randint(len(valid_idxs)) for the sample indices
+ *   v_pick / a_pick   randint(len(valid_idxs)) for random goals
+ *   v_geom / a_geom   geometric(1 - discount) offsets (geom mode)
+ *   v_dist / a_dist   rand() distances (uniform mode)
+ *   v_u_traj, v_u_cur, a_u_traj, a_u_cur   the two rand() of the where()s. */
+typedef struct {
+  const int64_t* idxs;  /* explicit sample indices (sample(idxs=...)) or NULL */
+  const int64_t* pick;
+  const int64_t* v_pick;
+  const int64_t* v_geom;
+  const double* v_dist;
+  const double* v_u_traj;
+  const double* v_u_cur;
+  const int64_t* a_pick;
+  const int64_t* a_geom;
+  const double* a_dist;
+  const double* a_u_traj;
+  const double* a_u_cur;
+} ogbx_gc_draws;
+
+/* Optional record of every draw the kernel used (same layout as
+ * ogbx_gc_draws, all non-NULL device buffers) so a checker can replay it. */
+typedef struct {
+  int64_t* pick;
+  int64_t* v_pick;
+  int64_t* v_geom;
+  double* v_dist;
+  double* v_u_traj;
+  double* v_u_cur;
+  int64_t* a_pick;
+  int64_t* a_geom;
+  double* a_dist;
+  double* a_u_traj;
+  double* a_u_cur;
+} ogbx_gc_draw_record;
+
+/* Sample num_batches x batch transitions with value/actor goals in ONE launch.
+ * Outputs: the columns (dst pointers), idxs_out / value_goal_out /
+ * actor_goal_out (device int64 [nb*B], each nullable), masks / rewards
+ * (device float64 [nb*B]: masks = 1 - (idxs == value_goal),
+ *  rewards = (idxs == value_goal) - gc_negative, datasets.py:250-252).
+ * Philox draws are keyed by (seed, stream tag) with counter (sample, call). */
+ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                           const ogbx_gc_column* cols, int32_t num_cols, int64_t batch,
+                           int64_t num_batches, const ogbx_gc_draws* draws, uint64_t seed,
+                           uint64_t call_index, int64_t* idxs_out, int64_t* value_goal_out,
+                           int64_t* actor_goal_out, double* masks, double* rewards,
+                           const ogbx_gc_draw_record* record, void* stream);
+
+/* traj_end[r] = terminal_locs[searchsorted(terminal_locs, r, 'left')] for
+ * r in [0, R): binary search per row over the sorted terminal_locs
+ * (device int64 [num_terminals]).  datasets.py:186,309. */
+ogbx_status ogbx_gc_traj_end(const int64_t* terminal_locs, int64_t num_terminals,
+                             int64_t num_rows, int64_t* traj_end, void* stream);
+
+/* out = nonzero(x > 0) for device float32 x[n] (stable order); *count is a
+ * device int64.  Used for valid_idxs / terminal_locs (datasets.py:59-60,185). */
+ogbx_status ogbx_nonzero_f32(const float* x, int64_t n, int64_t* out, int64_t* count,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

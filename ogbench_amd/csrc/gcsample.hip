@@ -1,0 +1,267 @@
+// gcsample.hip -- offline replay on gfx950: one fused launch draws the sample
+// indices, relabels value/actor goals in hindsight and gathers every dataset
+// column of the batch from the HBM-resident trajectory buffer.
+//
+// Reference (hliuson/ogbench):
+//   Dataset.get_random_idxs / get_subset   impls/utils/datasets.py:65-83
+//   GCDataset.sample                       impls/utils/datasets.py:213-294
+//   GCDataset.sample_goals                 impls/utils/datasets.py:296-327
+//
+// Layout: every column is a dense [R, row_bytes] device array (torch tensor).
+// One workgroup handles a tile of TB samples: lanes 0..TB-1 compute the four
+// row selectors of their sample into LDS, then all 256 lanes stream the rows
+// of every column (widest aligned unit: 16, 8 or 4 bytes) into the batch.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+
+#include "common.h"
+
+namespace ogbx {
+
+constexpr int kGcMaxTile = 64;
+constexpr int kGcMaxCols = 32;
+
+struct GcColumns {
+  ogbx_gc_column c[kGcMaxCols];
+};
+
+__device__ inline uint64_t bounded64(uint32_t hi, uint32_t lo, uint64_t n) {
+  const uint64_t u = ((uint64_t)hi << 32) | lo;
+  return __umul64hi(u, n);
+}
+
+struct GoalDraws {
+  int64_t pick;
+  int64_t geom;
+  double dist, u_traj, u_cur;
+};
+
+// GCDataset.sample_goals for one sample (datasets.py:296-327).
+__device__ inline int64_t sample_goal(int64_t idx, int64_t final_idx, const GoalDraws& d,
+                                      const int64_t* valid_idxs, int64_t num_valid,
+                                      double p_cur, double thresh, int geom, int cur_is_one) {
+  if (cur_is_one) return idx;
+  const int64_t rand_goal = valid_idxs ? valid_idxs[d.pick] : d.pick;
+  int64_t traj;
+  if (geom) {
+    const int64_t s = idx + d.geom;
+    traj = s < final_idx ? s : final_idx;
+  } else {
+    const int64_t lo = idx + 1 < final_idx ? idx + 1 : final_idx;
+    traj = (int64_t)rint((double)lo * d.dist + (double)final_idx * (1.0 - d.dist));
+  }
+  int64_t goal = d.u_traj < thresh ? traj : rand_goal;
+  goal = d.u_cur < p_cur ? idx : goal;
+  return goal;
+}
+
+__device__ inline int64_t geometric_from(double u, double log_q) {
+  // legacy RandomState.geometric inversion: ceil(log(1-u) / log(1-p))
+  double g = ceil(log(1.0 - u) / log_q);
+  return g < 1.0 ? 1 : (int64_t)g;
+}
+
+template <typename T>
+__device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, int64_t base,
+                                 int tile) {
+  const int64_t units = col.row_bytes / (int64_t)sizeof(T);
+  const T* __restrict__ src = (const T*)col.src;
+  T* __restrict__ dst = (T*)col.dst;
+  const int64_t total = units * tile;
+  const int step = blockDim.x;
+  int64_t b = threadIdx.x / units, k = threadIdx.x % units;
+  const int64_t sb = step / units, sk = step % units;
+  for (int64_t f = threadIdx.x; f < total; f += step) {
+    dst[(base + b) * units + k] = src[sel[b] * units + k];
+    k += sk;
+    b += sb;
+    if (k >= units) {
+      k -= units;
+      b += 1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) gc_sample_kernel(
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, GcColumns cols, int32_t num_cols, int64_t total,
+    int tile, ogbx_gc_draws dr, uint32_t k0, uint32_t k1, uint32_t call_lo, uint32_t call_hi,
+    double v_log_q, double a_log_q, int64_t* idxs_out, int64_t* vgoal_out, int64_t* agoal_out,
+    double* masks, double* rewards, ogbx_gc_draw_record rec) {
+  __shared__ int64_t sel[4][kGcMaxTile];
+  const int64_t base = (int64_t)blockIdx.x * tile;
+  int n_here = (int)((total - base) < tile ? (total - base) : tile);
+  if (threadIdx.x < n_here) {
+    const int64_t s = base + threadIdx.x;
+    const uint64_t su = (uint64_t)s;
+    const uint32_t c0 = (uint32_t)su, c3 = (uint32_t)(su >> 32) ^ call_hi;
+    const u32x4 w0 = philox4x32_10({c0, call_lo, 0u, c3}, k0, k1);
+    const u32x4 w1 = philox4x32_10({c0, call_lo, 1u, c3}, k0, k1);
+    const u32x4 w2 = philox4x32_10({c0, call_lo, 2u, c3}, k0, k1);
+    const u32x4 w3 = philox4x32_10({c0, call_lo, 3u, c3}, k0, k1);
+    const u32x4 w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
+    const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
+    // sample index (datasets.py:65-70)
+    int64_t idx, pick = -1;
+    if (dr.idxs) {
+      idx = dr.idxs[s];
+    } else {
+      pick = dr.pick ? dr.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
+      idx = buf.valid_idxs ? buf.valid_idxs[pick] : pick;
+    }
+    const int64_t final_idx = buf.traj_end[idx];
+    const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
+    GoalDraws v, a;
+    v.pick = dr.v_pick ? dr.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
+    a.pick = dr.a_pick ? dr.a_pick[s] : (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+    const double uvg = u01_from(w1.z, w1.w), uag = u01_from(w2.x, w2.y);
+    v.geom = dr.v_geom ? dr.v_geom[s] : (cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0);
+    a.geom = dr.a_geom ? dr.a_geom[s] : (cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0);
+    v.dist = dr.v_dist ? dr.v_dist[s] : uvg;
+    a.dist = dr.a_dist ? dr.a_dist[s] : uag;
+    v.u_traj = dr.v_u_traj ? dr.v_u_traj[s] : u01_from(w2.z, w2.w);
+    v.u_cur = dr.v_u_cur ? dr.v_u_cur[s] : u01_from(w3.x, w3.y);
+    a.u_traj = dr.a_u_traj ? dr.a_u_traj[s] : u01_from(w3.z, w3.w);
+    a.u_cur = dr.a_u_cur ? dr.a_u_cur[s] : u01_from(w4.x, w4.y);
+    const int64_t vg = sample_goal(idx, final_idx, v, buf.valid_idxs, buf.num_valid,
+                                   cfg.value_p_curgoal, cfg.value_traj_thresh,
+                                   cfg.value_geom_sample, cfg.value_cur_is_one);
+    const int64_t ag = sample_goal(idx, final_idx, a, buf.valid_idxs, buf.num_valid,
+                                   cfg.actor_p_curgoal, cfg.actor_traj_thresh,
+                                   cfg.actor_geom_sample, cfg.actor_cur_is_one);
+    sel[0][threadIdx.x] = idx;
+    sel[1][threadIdx.x] = next;
+    sel[2][threadIdx.x] = vg;
+    sel[3][threadIdx.x] = ag;
+    if (idxs_out) idxs_out[s] = idx;
+    if (vgoal_out) vgoal_out[s] = vg;
+    if (agoal_out) agoal_out[s] = ag;
+    const double succ = idx == vg ? 1.0 : 0.0;
+    masks[s] = 1.0 - succ;
+    rewards[s] = succ - (cfg.gc_negative ? 1.0 : 0.0);
+    if (rec.pick) {
+      rec.pick[s] = pick;
+      rec.v_pick[s] = v.pick;
+      rec.v_geom[s] = v.geom;
+      rec.v_dist[s] = v.dist;
+      rec.v_u_traj[s] = v.u_traj;
+      rec.v_u_cur[s] = v.u_cur;
+      rec.a_pick[s] = a.pick;
+      rec.a_geom[s] = a.geom;
+      rec.a_dist[s] = a.dist;
+      rec.a_u_traj[s] = a.u_traj;
+      rec.a_u_cur[s] = a.u_cur;
+    }
+  }
+  __syncthreads();
+  for (int c = 0; c < num_cols; ++c) {
+    const ogbx_gc_column& col = cols.c[c];
+    const int64_t* srow = sel[col.select];
+    const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst;
+    if (col.row_bytes % 16 == 0 && align % 16 == 0)
+      copy_rows<uint4>(col, srow, base, n_here);
+    else if (col.row_bytes % 8 == 0 && align % 8 == 0)
+      copy_rows<uint2>(col, srow, base, n_here);
+    else if (col.row_bytes % 4 == 0 && align % 4 == 0)
+      copy_rows<uint32_t>(col, srow, base, n_here);
+    else
+      copy_rows<uint8_t>(col, srow, base, n_here);
+  }
+}
+
+__global__ void traj_end_kernel(const int64_t* __restrict__ term, int64_t nterm, int64_t nrows,
+                                int64_t* __restrict__ out) {
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  // searchsorted(term, r, side='left'): first position with term[pos] >= r
+  int64_t lo = 0, hi = nterm;
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (term[mid] < r) lo = mid + 1;
+    else hi = mid;
+  }
+  out[r] = lo < nterm ? term[lo] : term[nterm - 1];
+}
+
+struct PositiveF32 {
+  const float* x;
+  __device__ bool operator()(const int64_t& i) const { return x[i] > 0.0f; }
+};
+
+}  // namespace ogbx
+
+using namespace ogbx;
+
+extern "C" {
+
+ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                           const ogbx_gc_column* cols, int32_t num_cols, int64_t batch,
+                           int64_t num_batches, const ogbx_gc_draws* draws, uint64_t seed,
+                           uint64_t call_index, int64_t* idxs_out, int64_t* value_goal_out,
+                           int64_t* actor_goal_out, double* masks, double* rewards,
+                           const ogbx_gc_draw_record* record, void* stream) {
+  OGBX_CHECK(buf && cfg && masks && rewards, OGBX_EINVAL, "ogbx_gc_sample: null argument");
+  OGBX_CHECK(num_cols >= 0 && num_cols <= kGcMaxCols, OGBX_EINVAL,
+             "ogbx_gc_sample: at most 32 columns");
+  OGBX_CHECK(batch > 0 && num_batches > 0, OGBX_EINVAL, "batch and num_batches must be > 0");
+  OGBX_CHECK(buf->num_rows > 0 && buf->traj_end, OGBX_EINVAL, "empty trajectory buffer");
+  OGBX_CHECK(buf->valid_idxs == nullptr || buf->num_valid > 0, OGBX_EINVAL,
+             "no valid transitions in the dataset");
+  GcColumns cc{};
+  for (int i = 0; i < num_cols; ++i) {
+    OGBX_CHECK(cols[i].src && cols[i].dst && cols[i].row_bytes > 0 && cols[i].select >= 0 &&
+                   cols[i].select <= 3,
+               OGBX_EINVAL, "ogbx_gc_sample: bad column descriptor");
+    cc.c[i] = cols[i];
+  }
+  ogbx_gc_draws dr{};
+  if (draws) dr = *draws;
+  ogbx_gc_draw_record rec{};
+  if (record) rec = *record;
+  const int64_t total = batch * num_batches;
+  // tile: enough workgroups to cover every CU (>= 512 when possible)
+  int64_t tile = total / 512;
+  if (tile < 1) tile = 1;
+  if (tile > kGcMaxTile) tile = kGcMaxTile;
+  const int64_t blocks = (total + tile - 1) / tile;
+  uint32_t k0, k1;
+  seed_key(seed, kTagGcSample, &k0, &k1);
+  const double v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
+  const double a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
+  hipLaunchKernelGGL(gc_sample_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
+                     *buf, *cfg, cc, num_cols, total, (int)tile, dr, k0, k1,
+                     (uint32_t)call_index, (uint32_t)(call_index >> 32), v_log_q, a_log_q,
+                     idxs_out, value_goal_out, actor_goal_out, masks, rewards, rec);
+  OGBX_LAUNCHED("gc_sample_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_gc_traj_end(const int64_t* terminal_locs, int64_t num_terminals,
+                             int64_t num_rows, int64_t* traj_end, void* stream) {
+  OGBX_CHECK(terminal_locs && traj_end && num_terminals > 0 && num_rows > 0, OGBX_EINVAL,
+             "ogbx_gc_traj_end: bad argument");
+  hipLaunchKernelGGL(traj_end_kernel, dim3((uint32_t)((num_rows + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, terminal_locs, num_terminals, num_rows, traj_end);
+  OGBX_LAUNCHED("traj_end_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_nonzero_f32(const float* x, int64_t n, int64_t* out, int64_t* count,
+                             void* stream) {
+  OGBX_CHECK(x && out && count && n >= 0, OGBX_EINVAL, "ogbx_nonzero_f32: bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  hipcub::CountingInputIterator<int64_t> it(0);
+  PositiveF32 pred{x};
+  size_t tmp_bytes = 0;
+  OGBX_HIP(hipcub::DeviceSelect::If(nullptr, tmp_bytes, it, out, count, n, pred, s));
+  void* tmp = nullptr;
+  OGBX_HIP(hipMallocAsync(&tmp, tmp_bytes > 0 ? tmp_bytes : 1, s));
+  hipError_t e = hipcub::DeviceSelect::If(tmp, tmp_bytes, it, out, count, n, pred, s);
+  hipError_t e2 = hipFreeAsync(tmp, s);
+  if (e != hipSuccess) return hip_fail(e, "hipcub::DeviceSelect::If");
+  if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync");
+  return OGBX_OK;
+}
+
+}  // extern "C"

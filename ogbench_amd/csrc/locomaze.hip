@@ -40,6 +40,7 @@ struct MazeParams {
   double tp_out[3][2];
   int32_t tasks[kMaxTasks][4];  // init_i, init_j, goal_i, goal_j
   uint8_t wall[kMaxCells];
+  uint16_t nbmask[kMaxCells];   // 3x3 wall mask per cell, bit (di+1)*3+(dj+1)
 };
 
 struct MazeState {
@@ -69,6 +70,11 @@ namespace ogbx {
 
 __device__ inline void stage_wall(const MazeParams& P, uint8_t* wall_s) {
   for (int t = threadIdx.x; t < P.H * P.W; t += blockDim.x) wall_s[t] = P.wall[t];
+  __syncthreads();
+}
+
+__device__ inline void stage_nbmask(const MazeParams& P, uint16_t* nb_s) {
+  for (int t = threadIdx.x; t < P.H * P.W; t += blockDim.x) nb_s[t] = P.nbmask[t];
   __syncthreads();
 }
 
@@ -180,8 +186,8 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     double* __restrict__ final_obs, int32_t auto_reset, uint32_t k0, uint32_t k1) {
   const MazeParams& P = *Pp;
   const PointModel pm = P.pm;
-  __shared__ uint8_t wall_s[kMaxCells];
-  stage_wall(P, wall_s);
+  __shared__ uint16_t nb_s[kMaxCells];
+  stage_nbmask(P, nb_s);
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
 
@@ -208,7 +214,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     if (P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
     x = x + dx;
     y = y + dy;
-    point_step(pm, wall_s, P.H, P.W, &x, &y);
+    point_step(pm, nb_s, P.H, P.W, &x, &y);
     if (!P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
     const double ox = x, oy = y;  // ob is taken before a teleport (maze.py:437-451)
     if (P.n_tp_in > 0) {
@@ -259,8 +265,8 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
                                                             uint8_t* contact_out) {
   const MazeParams& P = *Pp;
   const PointModel pm = P.pm;
-  __shared__ uint8_t wall_s[kMaxCells];
-  stage_wall(P, wall_s);
+  __shared__ uint16_t nb_s[kMaxCells];
+  stage_nbmask(P, nb_s);
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double x = qpos_in[2 * i], y = qpos_in[2 * i + 1];
@@ -273,7 +279,7 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
     x = x + (double)(0.2f * a[2 * i]);
     y = y + (double)(0.2f * a[2 * i + 1]);
   }
-  int c = point_step(pm, wall_s, P.H, P.W, &x, &y);
+  int c = point_step(pm, nb_s, P.H, P.W, &x, &y);
   qpos_out[2 * i] = x;
   qpos_out[2 * i + 1] = y;
   if (contact_out) contact_out[i] = (uint8_t)c;
@@ -537,6 +543,17 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
   P.max_steps = opts->max_episode_steps;
   P.goal_tol = opts->loco_type == 0 ? 1.0 : 0.5;  // maze.py:86
   for (int c = 0; c < spec->H * spec->W; ++c) P.wall[c] = spec->rows[c] == '1';
+  for (int i = 0; i < spec->H; ++i)
+    for (int j = 0; j < spec->W; ++j) {
+      uint16_t m = 0;
+      for (int di = -1; di <= 1; ++di)
+        for (int dj = -1; dj <= 1; ++dj) {
+          const int ii = i + di, jj = j + dj;
+          if (ii >= 0 && ii < spec->H && jj >= 0 && jj < spec->W && P.wall[ii * spec->W + jj])
+            m |= (uint16_t)(1u << ((di + 1) * 3 + (dj + 1)));
+        }
+      P.nbmask[i * spec->W + j] = m;
+    }
   for (int t = 0; t < spec->ntasks; ++t)
     for (int k = 0; k < 4; ++k) P.tasks[t][k] = spec->tasks[t][k];
   if (std::strcmp(spec->name, "teleport") == 0) {  // maze.py:151-161
@@ -598,6 +615,17 @@ ogbx_status ogbx_maze_destroy(ogbx_maze_t e) {
 }
 
 int64_t ogbx_maze_num_envs(ogbx_maze_t e) { return e ? e->n : 0; }
+
+#ifdef OGBX_PHYS_STATS
+// Diagnostic build only: read and clear the physics path counters.
+ogbx_status ogbx_diag_phys_stats(unsigned long long* out8) {
+  OGBX_HIP(hipDeviceSynchronize());
+  OGBX_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_phys_stats), 8 * sizeof(unsigned long long)));
+  unsigned long long z[8] = {0};
+  OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phys_stats), z, sizeof(z)));
+  return OGBX_OK;
+}
+#endif
 
 ogbx_status ogbx_maze_static_tables(const char* maze_type, int32_t* map_h, int32_t* map_w,
                                     int32_t* num_tasks, int32_t* map_out, int32_t* tasks_out) {

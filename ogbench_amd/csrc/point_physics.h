@@ -59,63 +59,87 @@ struct PointModel {
 };
 
 constexpr double kMinVal = 1e-15;  // mjMINVAL
+
+#ifdef OGBX_PHYS_STATS
+// Diagnostic build only (-DOGBX_PHYS_STATS): per-path counters.
+__device__ unsigned long long g_phys_stats[8];
+#define OGBX_STAT(k) atomicAdd(&g_phys_stats[k], 1ull)
+#else
+#define OGBX_STAT(k) ((void)0)
+#endif
+
 // A sphere whose centre lies in an empty cell touches at most 3 wall boxes
 // (two faces + the corner box between them).  States with the centre deep in
 // a wall (contact through a box z face = two pseudo-contacts) are unreachable
 // from any reset; there, contacts beyond 3 are dropped.
 constexpr int kMaxContacts = 3;
 
-struct Contacts {
-  int n;
-  double nx[kMaxContacts], ny[kMaxContacts];  // Jn: gradient of dist (slide dofs)
-  double tx[kMaxContacts], ty[kMaxContacts];  // slide projection of the horizontal tangent
-  double kp[kMaxContacts];                    // K*imp*dist
-  double w[kMaxContacts];                     // D = 1/R of one edge
+struct ContactSlot {
+  double nx, ny;  // Jn: gradient of dist (slide dofs)
+  double tx, ty;  // slide projection of the horizontal tangent
+  double kp;      // K*imp*dist
+  double w;       // D = 1/R of one edge
 };
 
-// Store one contact into slot `slot` (static predicated writes keep Contacts
-// in VGPRs).  imp = MuJoCo getimpedance() with solimp power 2; beyond the
-// transition width it is dmax and D, K*imp are the precomputed constants.
-__device__ inline void add_contact(const PointModel& pm, Contacts& c, int slot, double dist,
-                                   double nx, double ny, double tx, double ty) {
-  double D, kp;
-  const double x = fabs(dist / pm.imp_width);
-  if (x >= 1.0) {
-    D = pm.w_max;
-    kp = pm.kp_max * dist;
-  } else {
-    double imp;
-    if (x <= 0.0) {
-      imp = pm.imp_dmin;
-    } else {
-      const double y = x <= pm.imp_mid ? pm.imp_a * (x * x) : 1.0 - pm.imp_b * ((1.0 - x) * (1.0 - x));
-      imp = pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
-    }
-    double R = (1.0 - imp) * pm.diag / imp;
-    if (R < kMinVal) R = kMinVal;
-    D = 1.0 / R;
-    kp = pm.K * imp * dist;
-  }
-#pragma unroll
-  for (int s = 0; s < kMaxContacts; ++s) {
-    if (s == slot) {
-      c.nx[s] = nx;
-      c.ny[s] = ny;
-      c.tx[s] = tx;
-      c.ty[s] = ty;
-      c.kp[s] = kp;
-      c.w[s] = D;
-    }
-  }
+// Three named slots, not an array: LLVM cannot turn a write to a runtime slot
+// into a dynamically indexed store, so the contacts never leave VGPRs.
+struct Contacts {
+  int n;
+  ContactSlot s0, s1, s2;
+};
+
+// Static slot access (k is a compile-time constant in every unrolled loop).
+__device__ __forceinline__ const ContactSlot& slot_of(const Contacts& c, int k) {
+  return k == 0 ? c.s0 : (k == 1 ? c.s1 : c.s2);
 }
 
-// Exact sphere-box test of wall cell (i, j) (MuJoCo sphere-box collision in
-// the box frame; boxes are axis aligned, margin 0).  Appends to `c` on contact.
-__device__ inline void collide_box(const PointModel& pm, double x, double y, int i, int j,
+// Store one contact into slot `slot`.  imp = MuJoCo getimpedance() with solimp
+// power 2; beyond the transition width it is dmax and D, K*imp are the
+// precomputed constants (the quotient dist/width is only formed near the
+// transition, where it decides the sigmoid).  Slot 0 (the common case) is a
+// direct write; slots 1..2 use static predicated writes (no scratch).
+__device__ __forceinline__ void add_contact(const PointModel& pm, Contacts& c, int slot, double dist,
+                                   double nx, double ny, double tx, double ty) {
+  double D = pm.w_max, kp = pm.kp_max * dist;
+  if (fabs(dist) < 2.0 * pm.imp_width) {
+    const double x = fabs(dist / pm.imp_width);
+    if (x < 1.0) {
+      double imp;
+      if (x <= 0.0) {
+        imp = pm.imp_dmin;
+      } else {
+        const double y = x <= pm.imp_mid ? pm.imp_a * (x * x) : 1.0 - pm.imp_b * ((1.0 - x) * (1.0 - x));
+        imp = pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
+      }
+      double R = (1.0 - imp) * pm.diag / imp;
+      if (R < kMinVal) R = kMinVal;
+      D = 1.0 / R;
+      kp = pm.K * imp * dist;
+    }
+  }
+  // Per-field selects (not branches): a branchy store would be merged by
+  // SimplifyCFG into one store through a selected address -> scratch.
+  auto put = [&](ContactSlot& d, bool on) {
+    d.nx = on ? nx : d.nx;
+    d.ny = on ? ny : d.ny;
+    d.tx = on ? tx : d.tx;
+    d.ty = on ? ty : d.ty;
+    d.kp = on ? kp : d.kp;
+    d.w = on ? D : d.w;
+  };
+  put(c.s0, slot == 0);
+  put(c.s1, slot == 1);
+  put(c.s2, slot == 2);
+}
+
+// Exact sphere-box test of the wall box centred at (cx, cy) (MuJoCo sphere-box
+// collision in the box frame; boxes are axis aligned, margin 0).  Appends to
+// `c` on contact.
+__device__ __forceinline__ void collide_box(const PointModel& pm, double x, double y, double cx, double cy,
                                    Contacts& c, int& nc) {
   const double hx = pm.box_hxy, hz = pm.box_hz;
-  const double px = x - (j * pm.unit - pm.off_x);
-  const double py = y - (i * pm.unit - pm.off_y);
+  const double px = x - cx;
+  const double py = y - cy;
   const double pz = pm.sphere_z - pm.box_cz;
   const double clx = px < -hx ? -hx : (px > hx ? hx : px);
   const double cly = py < -hx ? -hx : (py > hx ? hx : py);
@@ -175,43 +199,37 @@ __device__ inline void collide_box(const PointModel& pm, double x, double y, int
 // neighbourhood can be touched (r < maze_unit/2); a neighbour on side s is a
 // candidate only if the centre is within r (+1e-9 slack) of that side of its
 // own cell, so the exact test runs for <= 4 boxes instead of 9 and the result
-// equals the full scan.  `wall` is the map in LDS (row-major, 1 = wall).
-__device__ inline int collide_walls(const PointModel& pm, const uint8_t* wall, int H, int W,
+// equals the full scan.  `nbmask` (LDS) holds, per cell, the 9-bit wall mask of
+// its 3x3 neighbourhood (bit (di+1)*3 + (dj+1)); cells outside the map are 0.
+__device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_t* nbmask, int H, int W,
                                     double x, double y, Contacts& c) {
-#pragma unroll
-  for (int s = 0; s < kMaxContacts; ++s) {
-    c.nx[s] = 0.0; c.ny[s] = 0.0; c.tx[s] = 0.0; c.ty[s] = 0.0; c.kp[s] = 0.0; c.w[s] = 0.0;
-  }
   const double fi = floor((y + pm.off_y + 0.5 * pm.unit) * pm.inv_unit);
   const double fj = floor((x + pm.off_x + 0.5 * pm.unit) * pm.inv_unit);
-  const int i0 = (int)fi, j0 = (int)fj;
-  const double lx = x - (fj * pm.unit - pm.off_x);  // offset from own cell centre
-  const double ly = y - (fi * pm.unit - pm.off_y);
+  const double cx = fj * pm.unit - pm.off_x, cy = fi * pm.unit - pm.off_y;
+  const double lx = x - cx, ly = y - cy;  // offset from own cell centre
   const double reach = pm.box_hxy - pm.radius - 1e-9;
   const int sx = lx >= reach ? 1 : (lx <= -reach ? -1 : 0);
   const int sy = ly >= reach ? 1 : (ly <= -reach ? -1 : 0);
-  // candidate boxes packed 4 bits each: (di+1) | (dj+1) << 2; one exact test
-  // body in a rolled loop keeps the code (and the register file) small.
-  auto is_wall = [&](int i, int j) {
-    return i >= 0 && i < H && j >= 0 && j < W && wall[i * W + j] != 0;
-  };
-  uint32_t cand = 0, ncand = 0;
-  auto push = [&](int di, int dj) {
-    if (is_wall(i0 + di, j0 + dj)) {
-      cand |= (uint32_t)((di + 1) | ((dj + 1) << 2)) << (4 * ncand);
-      ++ncand;
-    }
-  };
-  push(0, 0);
-  if (sx != 0) push(0, sx);
-  if (sy != 0) push(sy, 0);
-  if (sx != 0 && sy != 0) push(sy, sx);
+  const bool inside = fi >= 0.0 && fi < (double)H && fj >= 0.0 && fj < (double)W;
+  uint32_t m = 0;
+  if (inside) m = nbmask[(int)fi * W + (int)fj];
+  else if (fi >= -1.0 && fi <= (double)H && fj >= -1.0 && fj <= (double)W) m = 0x1FFu;  // off-map: conservative
   int nc = 0;
-#pragma unroll 1
-  for (uint32_t k = 0; k < ncand; ++k) {
-    const uint32_t code = (cand >> (4 * k)) & 15u;
-    collide_box(pm, x, y, i0 + (int)(code & 3u) - 1, j0 + (int)(code >> 2) - 1, c, nc);
-  }
+  c.n = 0;
+  if (m == 0) return 0;
+  const double u = pm.unit;
+  auto wall_at = [&](int di, int dj) -> bool {
+    if (inside) return (m >> ((di + 1) * 3 + (dj + 1))) & 1u;
+    const double ii = fi + di, jj = fj + dj;  // slow path off the map
+    if (!(ii >= 0.0 && ii < (double)H && jj >= 0.0 && jj < (double)W)) return false;
+    const int ci = (int)ii, cj = (int)jj;
+    // the cell's own bit of its neighbourhood mask is bit 4
+    return (nbmask[ci * W + cj] >> 4) & 1u;
+  };
+  if (wall_at(0, 0)) collide_box(pm, x, y, cx, cy, c, nc);
+  if (sx != 0 && wall_at(0, sx)) collide_box(pm, x, y, cx + sx * u, cy, c, nc);
+  if (sy != 0 && wall_at(sy, 0)) collide_box(pm, x, y, cx, cy + sy * u, c, nc);
+  if (sx != 0 && sy != 0 && wall_at(sy, sx)) collide_box(pm, x, y, cx + sx * u, cy + sy * u, c, nc);
   c.n = nc;
   return nc;
 }
@@ -227,11 +245,11 @@ __device__ inline int collide_walls(const PointModel& pm, const uint8_t* wall, i
 // {+}, {-}, {0,+}, {0,-}, {0,+,-} ({0} alone and {+,-} without 0 are
 // infeasible); each is a closed-form 2x2 solve and exactly one is consistent.
 // Returns false if rounding leaves none consistent (caller falls back).
-__device__ inline bool solve_one_contact(const PointModel& pm, const Contacts& c, double cux,
+__device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Contacts& c, double cux,
                                          double cuy, double* ux, double* uy) {
   const double M = pm.M;
-  const double nx = c.nx[0], ny = c.ny[0], tx = c.tx[0], ty = c.ty[0];
-  const double e = c.kp[0], w = c.w[0];
+  const double nx = c.s0.nx, ny = c.s0.ny, tx = c.s0.tx, ty = c.s0.ty;
+  const double e = c.s0.kp, w = c.s0.w;
   const double cn = nx * cux + ny * cuy, ct = tx * cux + ty * cuy;
   double un = cn, ut = ct;
   bool ok = true;
@@ -280,7 +298,7 @@ __device__ inline bool solve_one_contact(const PointModel& pm, const Contacts& c
 }
 
 // Residuals, gradient and Hessian of f at u.  Returns the active-edge mask.
-__device__ inline uint32_t eval_piece(const PointModel& pm, const Contacts& c, double cux,
+__device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Contacts& c, double cux,
                                       double cuy, double ux, double uy, double* g, double* h,
                                       double* fval) {
   const double M = pm.M;
@@ -292,16 +310,17 @@ __device__ inline uint32_t eval_piece(const PointModel& pm, const Contacts& c, d
 #pragma unroll
   for (int s = 0; s < kMaxContacts; ++s) {
     if (s < c.n) {
-      const double a = c.nx[s] * ux + c.ny[s] * uy + c.kp[s];
-      const double b = c.tx[s] * ux + c.ty[s] * uy;
+      const ContactSlot& k = slot_of(c, s);
+      const double a = k.nx * ux + k.ny * uy + k.kp;
+      const double b = k.tx * ux + k.ty * uy;
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
         const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
         const double r = e == 2 ? a : a + sg * b;
         if (r < 0.0) {
-          const double we = e == 2 ? 2.0 * c.w[s] : c.w[s];
-          const double jx = e == 2 ? c.nx[s] : c.nx[s] + sg * c.tx[s];
-          const double jy = e == 2 ? c.ny[s] : c.ny[s] + sg * c.ty[s];
+          const double we = e == 2 ? 2.0 * k.w : k.w;
+          const double jx = e == 2 ? k.nx : k.nx + sg * k.tx;
+          const double jy = e == 2 ? k.ny : k.ny + sg * k.ty;
           act |= 1u << (3 * s + e);
           g[0] += we * r * jx;
           g[1] += we * r * jy;
@@ -320,7 +339,7 @@ __device__ inline uint32_t eval_piece(const PointModel& pm, const Contacts& c, d
 // Several contacts: full-step semismooth Newton; u is optimal once the active
 // set at the Newton point equals the set the step was computed on.  Safety
 // net: damped Newton with Armijo backtracking (monotone, globally convergent).
-__device__ inline void solve_newton(const PointModel& pm, const Contacts& c, double cux,
+__device__ __forceinline__ void solve_newton(const PointModel& pm, const Contacts& c, double cux,
                                     double cuy, double* ux_io, double* uy_io) {
   double ux = *ux_io, uy = *uy_io;
   double g[2], h[3], f;
@@ -329,6 +348,7 @@ __device__ inline void solve_newton(const PointModel& pm, const Contacts& c, dou
 #pragma unroll 1
   for (int it = 0; it < 8; ++it) {
     const uint32_t act = eval_piece(pm, c, cux, cuy, ux, uy, g, h, &f);
+    OGBX_STAT(4);
     if (act == prev || (g[0] == 0.0 && g[1] == 0.0)) {
       done = true;
       break;
@@ -339,6 +359,7 @@ __device__ inline void solve_newton(const PointModel& pm, const Contacts& c, dou
     prev = act;
   }
   if (!done) {
+    OGBX_STAT(5);
     ux = cux;
     uy = cuy;
 #pragma unroll 1
@@ -365,13 +386,17 @@ __device__ inline void solve_newton(const PointModel& pm, const Contacts& c, dou
 }
 
 // qacc of the point mass at velocity (vx, vy) for the given wall contacts.
-__device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
+__device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
                                  double* ax_out, double* ay_out) {
   const double bvx = pm.B * vx, bvy = pm.B * vy;
   const double cux = pm.m_over_M * bvx, cuy = pm.m_over_M * bvy;  // floor-only minimiser
   double ux = cux, uy = cuy;
   bool solved = c.n == 0;
+  OGBX_STAT(c.n);
   if (c.n == 1) solved = solve_one_contact(pm, c, cux, cuy, &ux, &uy);
+#ifdef OGBX_ABLATE_NEWTON
+  if (!solved) solved = solve_one_contact(pm, c, cux, cuy, &ux, &uy), true;
+#endif
   if (!solved) solve_newton(pm, c, cux, cuy, &ux, &uy);
   *ax_out = ux - bvx;
   *ay_out = uy - bvy;
@@ -382,7 +407,7 @@ __device__ inline void solve_acc(const PointModel& pm, const Contacts& c, double
 // The 5 substeps x 4 RK stages run as one loop of 20 force evaluations so the
 // solver is instantiated once (mj_step -> mj_forward + mj_RungeKutta(N=4),
 // RK4_A = {1/2 ; 0, 1/2 ; 0, 0, 1}, RK4_B = {1/6, 1/3, 1/3, 1/6}).
-__device__ inline int point_step(const PointModel& pm, const uint8_t* wall, int H, int W,
+__device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* wall, int H, int W,
                                  double* px, double* py) {
   double x = *px, y = *py;
   Contacts c;
@@ -395,12 +420,19 @@ __device__ inline int point_step(const PointModel& pm, const uint8_t* wall, int 
   double vx = 0.0, vy = 0.0;                          // X[0] velocity of the substep
   double qsx = x, qsy = y, vsx = 0.0, vsy = 0.0;      // state of the current RK stage
   double sqx = 0.0, sqy = 0.0, svx = 0.0, svy = 0.0;  // B-weighted sums (dX)
+#ifdef OGBX_ABLATE_STAGES
+  const int nstage = OGBX_ABLATE_STAGES;
+#else
   const int nstage = 4 * pm.nsub;
+#endif
+  OGBX_STAT(6);
 #pragma unroll 1
   for (int e = 0; e < nstage; ++e) {
     const int st = e & 3;
     double fx, fy;
+#ifndef OGBX_ABLATE_COLLIDE
     if (e != 0) collide_walls(pm, wall, H, W, qsx, qsy, c);
+#endif
     solve_acc(pm, c, vsx, vsy, &fx, &fy);
     const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
     sqx = sqx + b * vsx;
