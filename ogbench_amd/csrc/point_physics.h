@@ -336,9 +336,11 @@ __device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Conta
   return act;
 }
 
-// Several contacts: full-step semismooth Newton; u is optimal once the active
-// set at the Newton point equals the set the step was computed on.  Safety
-// net: damped Newton with Armijo backtracking (monotone, globally convergent).
+// Several contacts: full-step semismooth Newton from the warm start *u_io
+// (the previous RK stage's solution; the optimum is unique, so the start only
+// changes the iteration count).  u is optimal once the active set at the
+// Newton point equals the set the step was computed on.  Safety net: damped
+// Newton with Armijo backtracking from cu (monotone, globally convergent).
 __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contacts& c, double cux,
                                     double cuy, double* ux_io, double* uy_io) {
   double ux = *ux_io, uy = *uy_io;
@@ -386,18 +388,32 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
 }
 
 // qacc of the point mass at velocity (vx, vy) for the given wall contacts.
+// (wx, wy): warm start for the multi-contact Newton (previous stage's u);
+// on return it holds this stage's u.
 __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
-                                 double* ax_out, double* ay_out) {
+                                 double* ax_out, double* ay_out, double* wx, double* wy) {
   const double bvx = pm.B * vx, bvy = pm.B * vy;
   const double cux = pm.m_over_M * bvx, cuy = pm.m_over_M * bvy;  // floor-only minimiser
   double ux = cux, uy = cuy;
   bool solved = c.n == 0;
+  if (c.n >= 2) {
+    ux = *wx;
+    uy = *wy;
+  }
   OGBX_STAT(c.n);
   if (c.n == 1) solved = solve_one_contact(pm, c, cux, cuy, &ux, &uy);
 #ifdef OGBX_ABLATE_NEWTON
   if (!solved) solved = solve_one_contact(pm, c, cux, cuy, &ux, &uy), true;
 #endif
-  if (!solved) solve_newton(pm, c, cux, cuy, &ux, &uy);
+  if (!solved) {
+    if (c.n == 1) {  // closed form rejected by rounding: cold start
+      ux = cux;
+      uy = cuy;
+    }
+    solve_newton(pm, c, cux, cuy, &ux, &uy);
+  }
+  *wx = ux;
+  *wy = uy;
   *ax_out = ux - bvx;
   *ay_out = uy - bvy;
 }
@@ -420,6 +436,7 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
   double vx = 0.0, vy = 0.0;                          // X[0] velocity of the substep
   double qsx = x, qsy = y, vsx = 0.0, vsy = 0.0;      // state of the current RK stage
   double sqx = 0.0, sqy = 0.0, svx = 0.0, svy = 0.0;  // B-weighted sums (dX)
+  double wux = 0.0, wuy = 0.0;                        // solver warm start (u)
 #ifdef OGBX_ABLATE_STAGES
   const int nstage = OGBX_ABLATE_STAGES;
 #else
@@ -433,7 +450,7 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
 #ifndef OGBX_ABLATE_COLLIDE
     if (e != 0) collide_walls(pm, wall, H, W, qsx, qsy, c);
 #endif
-    solve_acc(pm, c, vsx, vsy, &fx, &fy);
+    solve_acc(pm, c, vsx, vsy, &fx, &fy, &wux, &wuy);
     const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
     sqx = sqx + b * vsx;
     sqy = sqy + b * vsy;
