@@ -80,6 +80,10 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
 ogbx_status ogbx_maze_destroy(ogbx_maze_t env);
 /* Number of envs of the handle. */
 int64_t ogbx_maze_num_envs(ogbx_maze_t env);
+/* Launch shape of the step/physics kernels: envs carried per 64-lane wave
+ * (8, 16, 32 or 64; default 32).  Performance knob only -- results are
+ * identical for every value (DESIGN.md "Latency-bound contact path"). */
+ogbx_status ogbx_maze_set_envs_per_wave(ogbx_maze_t env, int32_t epw);
 
 /* Static description: H, W of the map, number of tasks, goal_tol
  * (maze.py:86: 1.0 point / 0.5 ant+humanoid), maze_unit (4.0). */

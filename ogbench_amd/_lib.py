@@ -96,6 +96,7 @@ _SIGNATURES = {
     'ogbx_maze_create': (c_int32, [c_char_p, c_int64, c_int32, P(MazeOpts), P(c_void_p)]),
     'ogbx_maze_destroy': (c_int32, [c_void_p]),
     'ogbx_maze_num_envs': (c_int64, [c_void_p]),
+    'ogbx_maze_set_envs_per_wave': (c_int32, [c_void_p, c_int32]),
     'ogbx_maze_describe': (c_int32, [c_void_p, P(c_int32), P(c_int32), P(c_int32), P(c_double), P(c_double)]),
     'ogbx_maze_tables': (c_int32, [c_void_p, c_void_p, c_void_p]),
     'ogbx_maze_static_tables': (c_int32, [c_char_p, P(c_int32), P(c_int32), P(c_int32), c_void_p, c_void_p]),

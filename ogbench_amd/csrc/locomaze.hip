@@ -62,6 +62,7 @@ struct ogbx_maze_env {
   int16_t* bfs = nullptr;  // [H*W goal cell][H*W cell] BFS distances (maze.py:517-536)
   uint64_t seed = 0;
   bool was_reset = false;
+  int epw = 32;  // envs per 64-lane wave of the step/physics kernels
 };
 
 namespace ogbx {
@@ -134,6 +135,18 @@ __device__ inline void reset_one(const MazeParams& P, int32_t task, const double
 
 // ------------------------------------------------------------------ kernels
 
+// Env index of this lane when each 64-lane wave carries only `epw` envs
+// (epw in {16, 32, 64}).  The contact path is a long fp64 dependency chain,
+// so one full wave per SIMD leaves the SIMD idle; fewer envs per wave (more
+// waves per SIMD) lets the SIMD interleave independent chains.  Returns -1 for
+// idle lanes.
+__device__ inline int64_t env_of_lane(int epw) {
+  const int lane = threadIdx.x & 63;
+  if (lane >= epw) return -1;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  return wave * epw + lane;
+}
+
 __global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __restrict__ Pp, MazeState S, int64_t n,
                                                          const int32_t* task_id,
                                                          const double* task_xy,
@@ -183,13 +196,13 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     int32_t k_steps,
     double* __restrict__ obs, float* __restrict__ reward, uint8_t* __restrict__ terminated,
     uint8_t* __restrict__ truncated, uint8_t* __restrict__ success,
-    double* __restrict__ final_obs, int32_t auto_reset, uint32_t k0, uint32_t k1) {
+    double* __restrict__ final_obs, int32_t auto_reset, uint32_t k0, uint32_t k1, int epw) {
   const MazeParams& P = *Pp;
   const PointModel pm = P.pm;
   __shared__ uint16_t nb_s[kMaxCells];
   stage_nbmask(P, nb_s);
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const int64_t i = env_of_lane(epw);
+  if (i < 0 || i >= n) return;
 
   double2 q = reinterpret_cast<const double2*>(S.qpos)[i];
   double2 g = reinterpret_cast<const double2*>(S.goal)[i];
@@ -262,13 +275,13 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
                                                             const double* qpos_in,
                                                             const void* action_v, int64_t n,
                                                             double* qpos_out,
-                                                            uint8_t* contact_out) {
+                                                            uint8_t* contact_out, int epw) {
   const MazeParams& P = *Pp;
   const PointModel pm = P.pm;
   __shared__ uint16_t nb_s[kMaxCells];
   stage_nbmask(P, nb_s);
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const int64_t i = env_of_lane(epw);
+  if (i < 0 || i >= n) return;
   double x = qpos_in[2 * i], y = qpos_in[2 * i + 1];
   if (kF64) {
     const double* a = (const double*)action_v;
@@ -616,6 +629,25 @@ ogbx_status ogbx_maze_destroy(ogbx_maze_t e) {
 
 int64_t ogbx_maze_num_envs(ogbx_maze_t e) { return e ? e->n : 0; }
 
+ogbx_status ogbx_maze_set_envs_per_wave(ogbx_maze_t e, int32_t epw) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(epw == 8 || epw == 16 || epw == 32 || epw == 64, OGBX_EINVAL,
+             "envs per wave must be 8, 16, 32 or 64");
+  e->epw = epw;
+  return OGBX_OK;
+}
+
+#ifdef OGBX_PHYS_STAMPS
+// Diagnostic build only: read and clear the per-wave stamp sums [4096][4].
+ogbx_status ogbx_diag_phys_stamps(unsigned long long* out) {
+  OGBX_HIP(hipDeviceSynchronize());
+  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phys_stamps), 4096 * 4 * sizeof(unsigned long long)));
+  static unsigned long long z[4096 * 4];
+  OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phys_stamps), z, sizeof(z)));
+  return OGBX_OK;
+}
+#endif
+
 #ifdef OGBX_PHYS_STATS
 // Diagnostic build only: read and clear the physics path counters.
 ogbx_status ogbx_diag_phys_stats(unsigned long long* out8) {
@@ -697,15 +729,16 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
   OGBX_HIP(hipSetDevice(e->device));
   uint32_t k0, k1;
   seed_key(e->seed, kTagMazeReset, &k0, &k1);
-  dim3 grid(grid_for(e->n, 256)), block(256);
+  const int epw = e->epw;
+  dim3 grid(grid_for(e->n * (64 / epw), 256)), block(256);
   if (action_is_f64)
     hipLaunchKernelGGL(maze_step_kernel<true>, grid, block, 0, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
-                       final_obs, auto_reset, k0, k1);
+                       final_obs, auto_reset, k0, k1, epw);
   else
     hipLaunchKernelGGL(maze_step_kernel<false>, grid, block, 0, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
-                       final_obs, auto_reset, k0, k1);
+                       final_obs, auto_reset, k0, k1, epw);
   OGBX_LAUNCHED("maze_step_kernel");
   return OGBX_OK;
 }
@@ -728,13 +761,14 @@ ogbx_status ogbx_point_physics(ogbx_maze_t e, const double* qpos_in, const void*
   OGBX_CHECK(e != nullptr && qpos_in && action && qpos_out, OGBX_EINVAL, "null argument");
   if (n <= 0) return OGBX_OK;
   OGBX_HIP(hipSetDevice(e->device));
-  dim3 grid(grid_for(n, 256)), block(256);
+  const int epw = e->epw;
+  dim3 grid(grid_for(n * (64 / epw), 256)), block(256);
   if (action_is_f64)
     hipLaunchKernelGGL(point_physics_kernel<true>, grid, block, 0, (hipStream_t)stream, e->Pd,
-                       qpos_in, action, n, qpos_out, contact_out);
+                       qpos_in, action, n, qpos_out, contact_out, epw);
   else
     hipLaunchKernelGGL(point_physics_kernel<false>, grid, block, 0, (hipStream_t)stream, e->Pd,
-                       qpos_in, action, n, qpos_out, contact_out);
+                       qpos_in, action, n, qpos_out, contact_out, epw);
   OGBX_LAUNCHED("point_physics_kernel");
   return OGBX_OK;
 }

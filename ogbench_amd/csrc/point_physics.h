@@ -60,6 +60,31 @@ struct PointModel {
 
 constexpr double kMinVal = 1e-15;  // mjMINVAL
 
+#ifdef OGBX_PHYS_STAMPS
+// Diagnostic build only: per-wave cycle sums of the stage-loop segments
+// [collide, solve, update, whole point_step], indexed by global wave id.
+__device__ unsigned long long g_phys_stamps[4096 * 4];
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define OGBX_STAMP_DECL unsigned long long _t0 = stamp(), _ta = 0, _tb = 0, _tc = 0, _tl = _t0, _tn;
+#define OGBX_STAMP_SEG(acc) do { _tn = stamp(); acc += _tn - _tl; _tl = _tn; } while (0)
+#define OGBX_STAMP_END do {                                                          \
+    const unsigned w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;               \
+    if ((threadIdx.x & 63) == 0 && w < 4096) {                                      \
+      atomicAdd(&g_phys_stamps[4 * w + 0], _ta); atomicAdd(&g_phys_stamps[4 * w + 1], _tb); \
+      atomicAdd(&g_phys_stamps[4 * w + 2], _tc);                                    \
+      atomicAdd(&g_phys_stamps[4 * w + 3], stamp() - _t0); } } while (0)
+#else
+#define OGBX_STAMP_DECL
+#define OGBX_STAMP_SEG(acc) ((void)0)
+#define OGBX_STAMP_END ((void)0)
+#endif
+
 #ifdef OGBX_PHYS_STATS
 // Diagnostic build only (-DOGBX_PHYS_STATS): per-path counters.
 __device__ unsigned long long g_phys_stats[8];
@@ -427,9 +452,11 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
                                  double* px, double* py) {
   double x = *px, y = *py;
   Contacts c;
+  OGBX_STAMP_DECL
   if (collide_walls(pm, wall, H, W, x, y, c) == 0) {
     *px = x + 0.0;
     *py = y + 0.0;
+    OGBX_STAMP_END;
     return 0;
   }
   const double h = pm.h;
@@ -450,7 +477,9 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
 #ifndef OGBX_ABLATE_COLLIDE
     if (e != 0) collide_walls(pm, wall, H, W, qsx, qsy, c);
 #endif
+    OGBX_STAMP_SEG(_ta);
     solve_acc(pm, c, vsx, vsy, &fx, &fy, &wux, &wuy);
+    OGBX_STAMP_SEG(_tb);
     const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
     sqx = sqx + b * vsx;
     sqy = sqy + b * vsy;
@@ -474,7 +503,9 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
       vsy = vy;
       sqx = sqy = svx = svy = 0.0;
     }
+    OGBX_STAMP_SEG(_tc);
   }
+  OGBX_STAMP_END;
   *px = x;
   *py = y;
   return 1;
