@@ -220,14 +220,73 @@ __device__ __forceinline__ void collide_box(const PointModel& pm, double x, doub
   ++nc;
 }
 
-// All wall contacts of the sphere at (x, y).  Only boxes of the 3x3
-// neighbourhood can be touched (r < maze_unit/2); a neighbour on side s is a
-// candidate only if the centre is within r (+1e-9 slack) of that side of its
-// own cell, so the exact test runs for <= 4 boxes instead of 9 and the result
-// equals the full scan.  `nbmask` (LDS) holds, per cell, the 9-bit wall mask of
-// its 3x3 neighbourhood (bit (di+1)*3 + (dj+1)); cells outside the map are 0.
-__device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_t* nbmask, int H, int W,
-                                    double x, double y, Contacts& c) {
+// Impedance-dependent (D, K*imp*dist) of a contact at `dist` (MuJoCo
+// getimpedance, solimp power 2).  Outside the transition width these are the
+// precomputed constants; `dist / width` is formed only near the transition.
+__device__ __forceinline__ void contact_gains(const PointModel& pm, double dist, double* D,
+                                              double* kp) {
+  *D = pm.w_max;
+  *kp = pm.kp_max * dist;
+  if (fabs(dist) < 2.0 * pm.imp_width) {
+    const double x = fabs(dist / pm.imp_width);
+    if (x < 1.0) {
+      double imp;
+      if (x <= 0.0) {
+        imp = pm.imp_dmin;
+      } else {
+        const double y = x <= pm.imp_mid ? pm.imp_a * (x * x) : 1.0 - pm.imp_b * ((1.0 - x) * (1.0 - x));
+        imp = pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
+      }
+      double R = (1.0 - imp) * pm.diag / imp;
+      if (R < kMinVal) R = kMinVal;
+      *D = 1.0 / R;
+      *kp = pm.K * imp * dist;
+    }
+  }
+}
+
+__device__ __forceinline__ void zero_slot(ContactSlot& k) {
+  k.nx = 0.0; k.ny = 0.0; k.tx = 0.0; k.ty = 0.0; k.kp = 0.0; k.w = 0.0;
+}
+
+// Generic (slow, rare) collision: the sphere centre is in a wall cell, off the
+// map, or exactly on a box face.  Same exact per-box test as the fast path.
+__device__ __forceinline__ int collide_walls_generic(const PointModel& pm, const uint16_t* nbmask,
+                                                  int H, int W, double x, double y, double fi,
+                                                  double fj, int sx, int sy, Contacts& c) {
+  zero_slot(c.s0);
+  zero_slot(c.s1);
+  zero_slot(c.s2);
+  const double cx = fj * pm.unit - pm.off_x, cy = fi * pm.unit - pm.off_y;
+  const double u = pm.unit;
+  auto wall_at = [&](int di, int dj) -> bool {
+    const double ii = fi + di, jj = fj + dj;
+    if (!(ii >= 0.0 && ii < (double)H && jj >= 0.0 && jj < (double)W)) return false;
+    return (nbmask[(int)ii * W + (int)jj] >> 4) & 1u;  // the cell's own wall bit
+  };
+  int nc = 0;
+  if (wall_at(0, 0)) collide_box(pm, x, y, cx, cy, c, nc);
+  if (sx != 0 && wall_at(0, sx)) collide_box(pm, x, y, cx + sx * u, cy, c, nc);
+  if (sy != 0 && wall_at(sy, 0)) collide_box(pm, x, y, cx, cy + sy * u, c, nc);
+  if (sx != 0 && sy != 0 && wall_at(sy, sx)) collide_box(pm, x, y, cx + sx * u, cy + sy * u, c, nc);
+  c.n = nc;
+  return nc;
+}
+
+// All wall contacts of the sphere at (x, y), branch-light.  Only boxes of the
+// 3x3 neighbourhood can be touched (r < maze_unit/2).  With the centre in an
+// empty cell the candidates have fixed roles and fixed slots:
+//   s0 = the x-side box (a face contact: ty == 0), s1 = the y-side box (face,
+//   tx == 0), s2 = the diagonal box (a vertical-edge contact: sqrt + division).
+// A neighbour on side s is a candidate only if the centre is within r (+1e-9
+// slack) of that side of its cell, so the result equals the full 9-box scan.
+// Face contacts use d = |t|, n = -sign(t): bit-identical to MuJoCo's
+// d = sqrt(t.t), n = -t/d because sqrt(fl(t*t)) == |t|.  Slots without a
+// contact are all-zero (their rows are inactive in every solver).
+// Rare geometry (centre in a wall cell / off the map / exactly on a face) is
+// routed to collide_walls_generic.
+__device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_t* nbmask, int H,
+                                             int W, double x, double y, Contacts& c) {
   const double fi = floor((y + pm.off_y + 0.5 * pm.unit) * pm.inv_unit);
   const double fj = floor((x + pm.off_x + 0.5 * pm.unit) * pm.inv_unit);
   const double cx = fj * pm.unit - pm.off_x, cy = fi * pm.unit - pm.off_y;
@@ -236,27 +295,86 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
   const int sx = lx >= reach ? 1 : (lx <= -reach ? -1 : 0);
   const int sy = ly >= reach ? 1 : (ly <= -reach ? -1 : 0);
   const bool inside = fi >= 0.0 && fi < (double)H && fj >= 0.0 && fj < (double)W;
-  uint32_t m = 0;
-  if (inside) m = nbmask[(int)fi * W + (int)fj];
-  else if (fi >= -1.0 && fi <= (double)H && fj >= -1.0 && fj <= (double)W) m = 0x1FFu;  // off-map: conservative
-  int nc = 0;
-  c.n = 0;
-  if (m == 0) return 0;
-  const double u = pm.unit;
-  auto wall_at = [&](int di, int dj) -> bool {
-    if (inside) return (m >> ((di + 1) * 3 + (dj + 1))) & 1u;
-    const double ii = fi + di, jj = fj + dj;  // slow path off the map
-    if (!(ii >= 0.0 && ii < (double)H && jj >= 0.0 && jj < (double)W)) return false;
-    const int ci = (int)ii, cj = (int)jj;
-    // the cell's own bit of its neighbourhood mask is bit 4
-    return (nbmask[ci * W + cj] >> 4) & 1u;
-  };
-  if (wall_at(0, 0)) collide_box(pm, x, y, cx, cy, c, nc);
-  if (sx != 0 && wall_at(0, sx)) collide_box(pm, x, y, cx + sx * u, cy, c, nc);
-  if (sy != 0 && wall_at(sy, 0)) collide_box(pm, x, y, cx, cy + sy * u, c, nc);
-  if (sx != 0 && sy != 0 && wall_at(sy, sx)) collide_box(pm, x, y, cx + sx * u, cy + sy * u, c, nc);
-  c.n = nc;
-  return nc;
+  const uint32_t m = inside ? nbmask[(int)fi * W + (int)fj] : 0x1FFu;
+  bool slow = !inside || ((m >> 4) & 1u);
+  const double hx = pm.box_hxy, r = pm.radius, u = pm.unit;
+  // role validity from the neighbourhood mask
+  const bool vX = sx != 0 && ((m >> (4 + sx)) & 1u);
+  const bool vY = sy != 0 && ((m >> (4 + 3 * sy)) & 1u);
+  const bool vD = sx != 0 && sy != 0 && ((m >> (4 + 3 * sy + sx)) & 1u);
+  // x-side box: centre (cx + sx u, cy)
+  double dX, tXx, tXy;
+  {
+    const double px = x - (cx + sx * u), py = y - cy;
+    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
+    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    tXx = clx - px;
+    tXy = cly - py;
+    dX = fabs(tXx);
+  }
+  double dY, tYx, tYy;
+  {
+    const double px = x - cx, py = y - (cy + sy * u);
+    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
+    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    tYx = clx - px;
+    tYy = cly - py;
+    dY = fabs(tYy);
+  }
+  double tDx, tDy, d2D;
+  {
+    const double px = x - (cx + sx * u), py = y - (cy + sy * u);
+    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
+    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    tDx = clx - px;
+    tDy = cly - py;
+    d2D = tDx * tDx + tDy * tDy;
+  }
+  const bool cX = vX && dX - r <= 0.0;
+  const bool cY = vY && dY - r <= 0.0;
+  bool cD = vD && d2D <= pm.r2_hi;
+  // exact-geometry guards: face roles must really be faces, d > mjMINVAL
+  slow = slow || (cX && (tXy != 0.0 || dX <= kMinVal)) || (cY && (tYx != 0.0 || dY <= kMinVal));
+  if (__builtin_expect(slow, 0)) return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
+  double dD = 0.0, nDx = 0.0, nDy = 0.0;
+  if (cD) {  // vertical-edge contact of the diagonal box
+    dD = sqrt(d2D);
+    if (dD - r > 0.0) {
+      cD = false;
+    } else if (dD <= kMinVal) {
+      return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
+    } else {
+      nDx = -tDx / dD;
+      nDy = -tDy / dD;
+    }
+  }
+  double D, kp;
+  // s0: x face, n = (-sign(tx), -ty) with ty = +-0
+  contact_gains(pm, dX - r, &D, &kp);
+  c.s0.nx = cX ? (tXx > 0.0 ? -1.0 : 1.0) : 0.0;
+  c.s0.ny = cX ? -tXy : 0.0;
+  c.s0.tx = -c.s0.ny;
+  c.s0.ty = c.s0.nx;
+  c.s0.kp = cX ? kp : 0.0;
+  c.s0.w = cX ? D : 0.0;
+  // s1: y face
+  contact_gains(pm, dY - r, &D, &kp);
+  c.s1.nx = cY ? -tYx : 0.0;
+  c.s1.ny = cY ? (tYy > 0.0 ? -1.0 : 1.0) : 0.0;
+  c.s1.tx = -c.s1.ny;
+  c.s1.ty = c.s1.nx;
+  c.s1.kp = cY ? kp : 0.0;
+  c.s1.w = cY ? D : 0.0;
+  // s2: diagonal box edge
+  contact_gains(pm, dD - r, &D, &kp);
+  c.s2.nx = cD ? nDx : 0.0;
+  c.s2.ny = cD ? nDy : 0.0;
+  c.s2.tx = -c.s2.ny;
+  c.s2.ty = c.s2.nx;
+  c.s2.kp = cD ? kp : 0.0;
+  c.s2.w = cD ? D : 0.0;
+  c.n = (int)cX + (int)cY + (int)cD;
+  return c.n;
 }
 
 // ---------------------------------------------------------------------------
@@ -273,8 +391,10 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
 __device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Contacts& c, double cux,
                                          double cuy, double* ux, double* uy) {
   const double M = pm.M;
-  const double nx = c.s0.nx, ny = c.s0.ny, tx = c.s0.tx, ty = c.s0.ty;
-  const double e = c.s0.kp, w = c.s0.w;
+  // exactly one slot is non-zero (the others are all-zero): sum them
+  const double nx = c.s0.nx + c.s1.nx + c.s2.nx, ny = c.s0.ny + c.s1.ny + c.s2.ny;
+  const double tx = c.s0.tx + c.s1.tx + c.s2.tx, ty = c.s0.ty + c.s1.ty + c.s2.ty;
+  const double e = c.s0.kp + c.s1.kp + c.s2.kp, w = c.s0.w + c.s1.w + c.s2.w;
   const double cn = nx * cux + ny * cuy, ct = tx * cux + ty * cuy;
   double un = cn, ut = ct;
   bool ok = true;
@@ -334,7 +454,7 @@ __device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Conta
   uint32_t act = 0;
 #pragma unroll
   for (int s = 0; s < kMaxContacts; ++s) {
-    if (s < c.n) {
+    {  // empty slots are all-zero: r = 0 is never < 0, so their rows are inactive
       const ContactSlot& k = slot_of(c, s);
       const double a = k.nx * ux + k.ny * uy + k.kp;
       const double b = k.tx * ux + k.ty * uy;
@@ -414,29 +534,30 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
 
 // qacc of the point mass at velocity (vx, vy) for the given wall contacts.
 // (wx, wy): warm start for the multi-contact Newton (previous stage's u);
-// on return it holds this stage's u.
-__device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& c, double vx, double vy,
-                                 double* ax_out, double* ay_out, double* wx, double* wy) {
+// on return it holds this stage's u.  The solver path is chosen per WAVE: if
+// any lane has >= 2 contacts every contact lane runs Newton (which also solves
+// single contacts exactly); otherwise the closed form runs.  One path per wave
+// and stage keeps SIMT from executing the union of both.
+__device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& c, double vx,
+                                          double vy, double* ax_out, double* ay_out, double* wx,
+                                          double* wy) {
   const double bvx = pm.B * vx, bvy = pm.B * vy;
   const double cux = pm.m_over_M * bvx, cuy = pm.m_over_M * bvy;  // floor-only minimiser
   double ux = cux, uy = cuy;
-  bool solved = c.n == 0;
-  if (c.n >= 2) {
-    ux = *wx;
-    uy = *wy;
-  }
   OGBX_STAT(c.n);
-  if (c.n == 1) solved = solve_one_contact(pm, c, cux, cuy, &ux, &uy);
+  bool need_newton;
+  if (__any(c.n >= 2)) {
+    need_newton = c.n >= 1;
+    ux = c.n >= 1 ? *wx : cux;
+    uy = c.n >= 1 ? *wy : cuy;
+  } else {
+    need_newton = false;
+    if (c.n == 1) need_newton = !solve_one_contact(pm, c, cux, cuy, &ux, &uy);
 #ifdef OGBX_ABLATE_NEWTON
-  if (!solved) solved = solve_one_contact(pm, c, cux, cuy, &ux, &uy), true;
+    need_newton = false;
 #endif
-  if (!solved) {
-    if (c.n == 1) {  // closed form rejected by rounding: cold start
-      ux = cux;
-      uy = cuy;
-    }
-    solve_newton(pm, c, cux, cuy, &ux, &uy);
   }
+  if (need_newton) solve_newton(pm, c, cux, cuy, &ux, &uy);
   *wx = ux;
   *wy = uy;
   *ax_out = ux - bvx;
