@@ -81,8 +81,9 @@ ogbx_status ogbx_maze_destroy(ogbx_maze_t env);
 /* Number of envs of the handle. */
 int64_t ogbx_maze_num_envs(ogbx_maze_t env);
 /* Launch shape of the step/physics kernels: envs carried per 64-lane wave
- * (8, 16, 32 or 64; default 32).  Performance knob only -- results are
- * identical for every value (DESIGN.md "Latency-bound contact path"). */
+ * (8, 16, 32 or 64; default 64).  Performance knob only: the contact solver
+ * path is chosen per wave, so results agree to solver rounding (~1e-15), not
+ * bit for bit, across values (DESIGN.md "Contact path on SIMT"). */
 ogbx_status ogbx_maze_set_envs_per_wave(ogbx_maze_t env, int32_t epw);
 
 /* Static description: H, W of the map, number of tasks, goal_tol

@@ -62,7 +62,7 @@ struct ogbx_maze_env {
   int16_t* bfs = nullptr;  // [H*W goal cell][H*W cell] BFS distances (maze.py:517-536)
   uint64_t seed = 0;
   bool was_reset = false;
-  int epw = 32;  // envs per 64-lane wave of the step/physics kernels
+  int epw = 64;  // envs per 64-lane wave of the step/physics kernels
 };
 
 namespace ogbx {

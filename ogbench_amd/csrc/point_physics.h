@@ -75,10 +75,10 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define OGBX_STAMP_SEG(acc) do { _tn = stamp(); acc += _tn - _tl; _tl = _tn; } while (0)
 #define OGBX_STAMP_END do {                                                          \
     const unsigned w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;               \
-    if ((threadIdx.x & 63) == 0 && w < 4096) {                                      \
-      atomicAdd(&g_phys_stamps[4 * w + 0], _ta); atomicAdd(&g_phys_stamps[4 * w + 1], _tb); \
-      atomicAdd(&g_phys_stamps[4 * w + 2], _tc);                                    \
-      atomicAdd(&g_phys_stamps[4 * w + 3], stamp() - _t0); } } while (0)
+    if (w < 4096) {                                                                 \
+      atomicMax(&g_phys_stamps[4 * w + 0], _ta); atomicMax(&g_phys_stamps[4 * w + 1], _tb); \
+      atomicMax(&g_phys_stamps[4 * w + 2], _tc);                                    \
+      atomicMax(&g_phys_stamps[4 * w + 3], stamp() - _t0); } } while (0)
 #else
 #define OGBX_STAMP_DECL
 #define OGBX_STAMP_SEG(acc) ((void)0)
