@@ -43,50 +43,6 @@ class MazeOpts(ctypes.Structure):
     ]
 
 
-class PowderOpts(ctypes.Structure):
-    _fields_ = [
-        ('world_size', c_int32),
-        ('grid_size', c_int32),
-        ('brush_size', c_int32),
-        ('num_elems', c_int32),
-        ('max_episode_steps', c_int32),
-        ('mode', c_int32),
-    ]
-
-
-class GcBuffer(ctypes.Structure):
-    _fields_ = [
-        ('num_rows', c_int64),
-        ('num_cols', c_int32),
-        ('pad_', c_int32),
-        ('col_ptr', c_void_p),
-        ('col_row_bytes', c_void_p),
-        ('terminal_locs', c_void_p),
-        ('num_terminals', c_int64),
-        ('valid_idxs', c_void_p),
-        ('num_valid', c_int64),
-        ('traj_end', c_void_p),
-        ('obs_col', c_int32),
-        ('goal_col', c_int32),
-    ]
-
-
-class GcConfig(ctypes.Structure):
-    _fields_ = [
-        ('discount', c_double),
-        ('value_p_curgoal', c_double),
-        ('value_p_trajgoal', c_double),
-        ('value_p_randomgoal', c_double),
-        ('actor_p_curgoal', c_double),
-        ('actor_p_trajgoal', c_double),
-        ('actor_p_randomgoal', c_double),
-        ('gc_negative', c_int32),
-        ('value_geom_sample', c_int32),
-        ('actor_geom_sample', c_int32),
-        ('pad_', c_int32),
-    ]
-
-
 # name -> (restype, argtypes)
 _SIGNATURES = {
     'ogbx_last_error': (c_char_p, []),

@@ -1,0 +1,344 @@
+"""HBM-resident offline datasets and the goal-conditioned sampler.
+
+Batched, device-side counterparts of impls/utils/datasets.py (hliuson/ogbench):
+
+  Dataset    ~ Dataset (datasets.py:36-83): a dict of device tensors with
+               ``size``, ``valid_idxs``, ``get_random_idxs``, ``sample``,
+               ``get_subset``;
+  GCDataset  ~ GCDataset (datasets.py:149-366): ``sample(batch_size, idxs=None,
+               evaluation=False)`` returns the same keys as the reference
+               (every dataset key, ``next_observations``, ``value_goals``,
+               ``actor_goals``, ``masks``, ``rewards``).
+
+Every sample is ONE launch of ``gc_sample_kernel`` (libogbx): index draw,
+trajectory-end lookup, hindsight goal relabel and the row gathers of every
+column are fused.  Random numbers come from a counter-based Philox stream
+(key = seed, counter = (sample, call)); the reference's NumPy draws can be
+injected bit-exactly through ``draws=`` for parity tests.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+class GcColumn(ctypes.Structure):
+    _fields_ = [
+        ('src', ctypes.c_void_p),
+        ('dst', ctypes.c_void_p),
+        ('row_bytes', ctypes.c_int64),
+        ('select', ctypes.c_int32),
+        ('pad_', ctypes.c_int32),
+    ]
+
+
+class GcBuffer(ctypes.Structure):
+    _fields_ = [
+        ('num_rows', ctypes.c_int64),
+        ('valid_idxs', ctypes.c_void_p),
+        ('num_valid', ctypes.c_int64),
+        ('traj_end', ctypes.c_void_p),
+    ]
+
+
+class GcConfig(ctypes.Structure):
+    _fields_ = [
+        ('value_p_curgoal', ctypes.c_double),
+        ('value_traj_thresh', ctypes.c_double),
+        ('value_discount', ctypes.c_double),
+        ('actor_p_curgoal', ctypes.c_double),
+        ('actor_traj_thresh', ctypes.c_double),
+        ('actor_discount', ctypes.c_double),
+        ('value_geom_sample', ctypes.c_int32),
+        ('actor_geom_sample', ctypes.c_int32),
+        ('value_cur_is_one', ctypes.c_int32),
+        ('actor_cur_is_one', ctypes.c_int32),
+        ('gc_negative', ctypes.c_int32),
+        ('pad_', ctypes.c_int32),
+    ]
+
+
+_DRAW_INT = ('pick', 'v_pick', 'v_geom', 'a_pick', 'a_geom')
+_DRAW_FLOAT = ('v_dist', 'v_u_traj', 'v_u_cur', 'a_dist', 'a_u_traj', 'a_u_cur')
+_DRAW_ORDER = ('pick', 'v_pick', 'v_geom', 'v_dist', 'v_u_traj', 'v_u_cur',
+               'a_pick', 'a_geom', 'a_dist', 'a_u_traj', 'a_u_cur')
+
+
+class GcDraws(ctypes.Structure):
+    _fields_ = [('idxs', ctypes.c_void_p)] + [(k, ctypes.c_void_p) for k in _DRAW_ORDER]
+
+
+class GcDrawRecord(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in _DRAW_ORDER]
+
+
+def _bind():
+    L = _lib.lib()
+    if not getattr(L, '_gc_bound', False):
+        P = ctypes.POINTER
+        L.ogbx_gc_sample.restype = ctypes.c_int32
+        L.ogbx_gc_sample.argtypes = [
+            P(GcBuffer), P(GcConfig), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+            P(GcDraws), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, P(GcDrawRecord), ctypes.c_void_p,
+        ]
+        L.ogbx_gc_traj_end.restype = ctypes.c_int32
+        L.ogbx_gc_traj_end.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                       ctypes.c_void_p]
+        L.ogbx_nonzero_f32.restype = ctypes.c_int32
+        L.ogbx_nonzero_f32.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p]
+        L._gc_bound = True
+    return L
+
+
+def nonzero_positive(x):
+    """nonzero(x > 0) of a float32 device vector, via the libogbx compaction."""
+    torch = _torch()
+    x = x.reshape(-1)
+    if x.dtype != torch.float32:
+        x = x.to(torch.float32)
+    x = x.contiguous()
+    L = _bind()
+    out = torch.empty(x.numel(), dtype=torch.int64, device=x.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=x.device)
+    _lib.check(L.ogbx_nonzero_f32(_lib.ptr(x), x.numel(), _lib.ptr(out), _lib.ptr(cnt),
+                                  _lib.stream_of(x.device)))
+    return out[: int(cnt.item())]
+
+
+def _to_device(v, device):
+    torch = _torch()
+    if isinstance(v, torch.Tensor):
+        t = v.to(device)
+    else:
+        t = torch.as_tensor(np.ascontiguousarray(v), device=device)
+    return t.contiguous()
+
+
+class Dataset(dict):
+    """Dataset of device tensors (reference: datasets.py:36-83).
+
+    Keys are kept in insertion order; arrays are moved to ``device`` once
+    (HBM-resident).  ``valid_idxs`` is computed on the device when 'valids'
+    exists (datasets.py:59-60).
+    """
+
+    @classmethod
+    def create(cls, freeze=True, device=None, **fields):
+        assert 'observations' in fields
+        return cls(fields, device=device)
+
+    def __init__(self, data=(), device=None, **kw):
+        torch = _torch()
+        data = dict(data, **kw)
+        if device is None:
+            first = next(iter(data.values()))
+            device = first.device if isinstance(first, torch.Tensor) and first.is_cuda else 'cuda'
+        self.device = torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device('cuda', torch.cuda.current_device())
+        super().__init__({k: _to_device(v, self.device) for k, v in data.items()})
+        self.size = max(len(v) for v in self.values())
+        if 'valids' in self:
+            self.valid_idxs = nonzero_positive(self['valids'])
+        self._seed = None
+        self._calls = 0
+
+    def copy(self, add_or_replace=None):
+        d = dict(self)
+        if add_or_replace:
+            d.update(add_or_replace)
+        return Dataset(d, device=self.device)
+
+    # the sampling entry points go through GCDataset's kernel with both goal
+    # relabels disabled (p_curgoal = 1 short-circuit, datasets.py:318-319)
+    def _sampler(self):
+        if getattr(self, '_plain_sampler', None) is None:
+            self._plain_sampler = GCDataset(self, _PLAIN_CONFIG, _plain=True)
+        return self._plain_sampler
+
+    def get_random_idxs(self, num_idxs):
+        """datasets.py:65-70 (Philox draws on the device)."""
+        return self._sampler().sample(num_idxs, _keys=())['_idxs']
+
+    def sample(self, batch_size, idxs=None):
+        out = self._sampler().sample(batch_size, idxs=idxs)
+        for k in ('value_goals', 'actor_goals', 'masks', 'rewards', '_idxs'):
+            out.pop(k, None)
+        return out
+
+    def get_subset(self, idxs):
+        return self.sample(len(idxs), idxs=idxs)
+
+
+_PLAIN_CONFIG = dict(
+    discount=0.99, value_p_curgoal=1.0, value_p_trajgoal=0.0, value_p_randomgoal=0.0, value_geom_sample=False,
+    actor_p_curgoal=1.0, actor_p_trajgoal=0.0, actor_p_randomgoal=0.0, actor_geom_sample=False,
+    gc_negative=False, p_aug=None, frame_stack=None,
+)
+
+
+class GCDataset:
+    """Goal-conditioned sampler (reference: datasets.py:149-366).
+
+    config keys read (as the reference): discount, value_/actor_ p_curgoal,
+    p_trajgoal, p_randomgoal, geom_sample, gc_negative, p_aug, frame_stack.
+    """
+
+    def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None, _plain=False):
+        torch = _torch()
+        if not isinstance(dataset, Dataset):
+            dataset = Dataset(dataset)
+        self.dataset = dataset
+        self.config = config
+        self.preprocess_frame_stack = preprocess_frame_stack
+        self.size = dataset.size
+        self.device = dataset.device
+        if config.get('frame_stack') is not None:
+            raise NotImplementedError('frame stacking (visual datasets) is out of scope')
+        if config.get('agent_name') in ('trl', 'latent_trl', 'discrete_latent_trl'):
+            raise NotImplementedError('the TRL sampling branches are out of scope')
+        L = _bind()
+        self._L = L
+        stream = _lib.stream_of(self.device)
+        if 'terminals' in dataset:
+            self.terminal_locs = nonzero_positive(dataset['terminals'])
+        else:
+            self.terminal_locs = torch.tensor([self.size - 1], dtype=torch.int64, device=self.device)
+        if not _plain:
+            assert self.terminal_locs.numel() > 0 and int(self.terminal_locs[-1]) == self.size - 1
+            assert np.isclose(
+                config['value_p_curgoal'] + config['value_p_trajgoal'] + config['value_p_randomgoal'], 1.0)
+            assert np.isclose(
+                config['actor_p_curgoal'] + config['actor_p_trajgoal'] + config['actor_p_randomgoal'], 1.0)
+        self.initial_locs = torch.cat([torch.zeros(1, dtype=torch.int64, device=self.device),
+                                       self.terminal_locs[:-1] + 1])
+        self.traj_end = torch.empty(self.size, dtype=torch.int64, device=self.device)
+        if self.terminal_locs.numel() > 0:
+            _lib.check(L.ogbx_gc_traj_end(_lib.ptr(self.terminal_locs), self.terminal_locs.numel(), self.size,
+                                          _lib.ptr(self.traj_end), stream))
+        else:
+            self.traj_end.fill_(self.size - 1)
+        valid = getattr(dataset, 'valid_idxs', None)
+        self._buf = GcBuffer(self.size, valid.data_ptr() if valid is not None else None,
+                             valid.numel() if valid is not None else 0, self.traj_end.data_ptr())
+        self._valid = valid
+
+        def thresh(p_traj, p_cur):
+            return p_traj / (1.0 - p_cur) if p_cur != 1.0 else 0.0  # datasets.py:321
+
+        c = config
+        self._cfg = GcConfig(
+            float(c['value_p_curgoal']), thresh(c['value_p_trajgoal'], c['value_p_curgoal']), float(c['discount']),
+            float(c['actor_p_curgoal']), thresh(c['actor_p_trajgoal'], c['actor_p_curgoal']), float(c['discount']),
+            int(bool(c['value_geom_sample'])), int(bool(c['actor_geom_sample'])),
+            int(c['value_p_curgoal'] == 1.0), int(c['actor_p_curgoal'] == 1.0), int(bool(c['gc_negative'])), 0,
+        )
+        self._seed = int(seed) if seed is not None else None
+        self._calls = 0
+        self._plain = _plain
+
+    # ---------------------------------------------------------------- helpers
+    def _next_seed(self):
+        if self._seed is None:
+            self._seed = int(np.random.randint(0, 2**63 - 1))
+        call = self._calls
+        self._calls += 1
+        return self._seed, call
+
+    def _columns(self, total, keys):
+        """Column descriptors and the output dict (reference key order)."""
+        torch = _torch()
+        ds = self.dataset
+        out, cols = {}, []
+
+        def add(src_key, dst_key, select):
+            src = ds[src_key]
+            dst = torch.empty((total,) + tuple(src.shape[1:]), dtype=src.dtype, device=self.device)
+            row_bytes = src[0].numel() * src.element_size() if src.dim() > 1 else src.element_size()
+            out[dst_key] = dst
+            cols.append(GcColumn(src.data_ptr(), dst.data_ptr(), row_bytes, select, 0))
+
+        for k in (ds.keys() if keys is None else keys):
+            add(k, k, 0)
+        if keys is None and 'next_observations' not in ds:
+            add('observations', 'next_observations', 1)  # datasets.py:81-82
+        if not self._plain and keys is None:
+            goal_src = 'oracle_reps' if 'oracle_reps' in ds else 'observations'  # datasets.py:348-357
+            add(goal_src, 'value_goals', 2)
+            add(goal_src, 'actor_goals', 3)
+        return out, cols
+
+    def sample(self, batch_size, idxs=None, evaluation=False, draws=None, record_draws=False,
+               num_batches=1, _keys=None):
+        """GCDataset.sample (datasets.py:213-294), one fused launch.
+
+        draws: optional dict of injected reference draws (see ``_DRAW_ORDER``;
+        device or host arrays of length num_batches*batch_size).
+        record_draws: also return the draws the kernel used (``out['_draws']``).
+        num_batches > 1: sample that many independent batches in the same launch
+        (outputs have a leading num_batches*batch_size dimension).
+        """
+        torch = _torch()
+        total = int(batch_size) * int(num_batches)
+        out, cols = self._columns(total, _keys)
+        col_arr = (GcColumn * max(1, len(cols)))(*cols)
+        masks = torch.empty(total, dtype=torch.float64, device=self.device)
+        rewards = torch.empty(total, dtype=torch.float64, device=self.device)
+        idx_out = torch.empty(total, dtype=torch.int64, device=self.device)
+        vg = torch.empty(total, dtype=torch.int64, device=self.device) if not self._plain else None
+        ag = torch.empty(total, dtype=torch.int64, device=self.device) if not self._plain else None
+        keep = []
+        dr = GcDraws()
+        if idxs is not None:
+            t = _to_device(idxs, self.device).to(torch.int64).reshape(-1)
+            assert t.numel() == total
+            keep.append(t)
+            dr.idxs = t.data_ptr()
+        if draws:
+            for k, v in draws.items():
+                if k == 'idxs':
+                    continue
+                dt = torch.int64 if k in _DRAW_INT else torch.float64
+                t = _to_device(v, self.device).to(dt).reshape(-1)
+                assert t.numel() == total, k
+                keep.append(t)
+                setattr(dr, k, t.data_ptr())
+        rec = None
+        rec_t = None
+        if record_draws:
+            rec_t = {k: torch.empty(total, dtype=torch.int64 if k in _DRAW_INT else torch.float64,
+                                    device=self.device) for k in _DRAW_ORDER}
+            rec = GcDrawRecord(*[rec_t[k].data_ptr() for k in _DRAW_ORDER])
+        seed, call = self._next_seed()
+        _lib.check(self._L.ogbx_gc_sample(
+            self._buf, self._cfg, ctypes.cast(col_arr, ctypes.c_void_p), len(cols), int(batch_size),
+            int(num_batches), dr, seed, call, _lib.ptr(idx_out), _lib.ptr(vg), _lib.ptr(ag), _lib.ptr(masks),
+            _lib.ptr(rewards), rec, _lib.stream_of(self.device)), 'gc_sample')
+        if self._plain:
+            out['_idxs'] = idx_out
+            return out
+        out['masks'] = masks
+        out['rewards'] = rewards
+        # p_aug draw (datasets.py:278-279): image crops apply only to 4-D arrays
+        p_aug = self.config.get('p_aug')
+        if p_aug is not None and not evaluation:
+            if np.random.rand() < p_aug and any(v.dim() == 4 for v in out.values()):
+                raise NotImplementedError('image augmentation (visual datasets) is out of scope')
+        if record_draws:
+            out['_draws'] = rec_t
+            out['_idxs'] = idx_out
+            out['_value_goal_idxs'] = vg
+            out['_actor_goal_idxs'] = ag
+        return out
