@@ -296,9 +296,10 @@ class GCDataset:
         col_arr = (GcColumn * max(1, len(cols)))(*cols)
         masks = torch.empty(total, dtype=torch.float64, device=self.device)
         rewards = torch.empty(total, dtype=torch.float64, device=self.device)
-        idx_out = torch.empty(total, dtype=torch.int64, device=self.device)
-        vg = torch.empty(total, dtype=torch.int64, device=self.device) if not self._plain else None
-        ag = torch.empty(total, dtype=torch.int64, device=self.device) if not self._plain else None
+        # index outputs only when asked for (plain sampling or draw recording)
+        idx_out = torch.empty(total, dtype=torch.int64, device=self.device) if (self._plain or record_draws) else None
+        vg = torch.empty(total, dtype=torch.int64, device=self.device) if record_draws else None
+        ag = torch.empty(total, dtype=torch.int64, device=self.device) if record_draws else None
         keep = []
         dr = GcDraws()
         if idxs is not None:
