@@ -304,12 +304,97 @@ def cpu_baseline_gc(data, cfg, B, args):
                 sample=f'{n} batches of {B} on the 1M-row humanoid buffer ({dt:.1f} s)')
 
 
+def bench_powder(args, world, rank, dev):
+    """powderworld-easy-v0, 64x64 worlds, N=4096 envs per GPU (SURVEY.md section 8 row b).
+    A step = one env.step of all envs (one pw_step_kernel launch), uniformly random
+    valid actions for the current stage, task i%5+1, same-step auto-reset."""
+    import ogbench_amd
+
+    n = 4096 if args.num_envs == 65536 else args.num_envs
+    size = 64
+    env = ogbench_amd.make('powderworld-easy-v0', num_envs=n, device=dev, world_size=size, auto_reset=True)
+    task = (torch.arange(n, dtype=torch.int32, device=dev) % 5) + 1
+    env.reset(seed=rank, options=dict(task_id=task))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5 + 1000 * rank)
+    ring = 3 * 32
+    xy = env._xy_action_size
+    hi = torch.tensor([2 if i % 3 == 0 else xy for i in range(ring)], device=dev).view(ring, 1)
+    actions = (torch.rand(ring, n, device=dev, generator=gen) * hi).to(torch.int32)
+
+    def step(i):
+        env.step(actions[i % ring])
+
+    for i in range(args.warmup):
+        step(i)
+    steps = args.steps - args.steps % 3 if args.steps >= 3 else args.steps
+    dt = _timed(step, steps, world, dev)
+    value = n * steps * world / dt
+    kern_ms = _per_launch_ms(step, min(steps, 201) - min(steps, 201) % 3 or 1, dev)
+    # algorithmic bytes per env-step: obs write H*W*6, world read H*W, world
+    # write H*W on one step in three, action 4, reward 4, flags 3, ctrl 16.
+    per_step = size * size * 6 + size * size + size * size / 3 + 27
+    achieved = per_step * n / (kern_ms * 1e-3) / 1e9
+    K = 48
+    fk_actions = actions[:K].contiguous()
+    out = None
+
+    def fused(i):
+        nonlocal out
+        out = env.rollout(fk_actions, out=out)
+
+    fused(0)
+    reps = max(1, steps // K)
+    fdt = _timed(fused, reps, world, dev)
+    fk_ms = _per_launch_ms(fused, 3, dev)
+    result = dict(
+        metric='env steps/sec, powderworld-easy-v0 64x64, N=4096 parallel envs per GPU',
+        value=value, unit='env_steps/s', n_gpus=world, steps=steps, warmup=args.warmup,
+        ms_per_step=dt / steps * 1e3, higher_is_better=True, scaling='weak', vs_baseline=None,
+        dtype='u8', data='synthetic (uniform valid Discrete actions per stage; Philox resets)',
+        config=dict(workload='powderworld-easy-v0 world_size=64', num_envs_per_gpu=n, auto_reset=True,
+                    parallelism=f'env-shard x{world}'),
+        roofline=dict(bound='hbm', kernel='pw_step_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
+                      frac=achieved / HBM_PEAK_GBS, traffic=None, kernel_ms=kern_ms,
+                      alg_bytes_per_launch=per_step * n),
+        extra=dict(fused_k48_steps_per_s=n * K * reps * world / fdt, fused_k48_kernel_ms=fk_ms,
+                   fused_k48_achieved_GBs=per_step * n * K / (fk_ms * 1e-3) / 1e9),
+    )
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline_powder(size, args)
+    env.close()
+    return result
+
+
+def cpu_baseline_powder(size, args):
+    """The NumPy oracle (kind 'port', 1 core): one env at a time, random valid actions."""
+    from oracle import powder_np as orc
+    from ogbench_amd.powder_tasks import easy_task_sequences
+
+    rng = np.random.RandomState(0)
+    o = orc.Env(size)
+    ids, grav, didg = o.blank()
+    for e, x, y in easy_task_sequences()[0]:
+        ids, grav, didg = orc.paint(*orc.forward(ids, grav, didg), orc.EASY_ELEMS[e], x, y)
+    o.reset(ids, 0, 3, 3)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        a = rng.randint(0, 2 if o.stage == 0 else o.xy)
+        _, _, succ = o.step(int(a))
+        n += 1
+        if succ or n % 500 == 0:
+            o.reset(ids, rng.randint(2), rng.randint(o.xy), rng.randint(o.xy))
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit='env_steps/s', cores=1, kind='port',
+                sample=f'{n} single-env steps of powderworld-easy {size}x{size} ({dt:.1f} s)')
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=100)
-    ap.add_argument('--workload', default='pointmaze', choices=['pointmaze', 'gcsample'])
+    ap.add_argument('--workload', default='pointmaze', choices=['pointmaze', 'powder', 'gcsample'])
     ap.add_argument('--num-envs', type=int, default=65536)
     ap.add_argument('--ring', type=int, default=128)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -322,7 +407,7 @@ def main():
     import sys
 
     sys.path.insert(0, ROOT)
-    fn = dict(pointmaze=bench_pointmaze, gcsample=bench_gcsample)[args.workload]
+    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, gcsample=bench_gcsample)[args.workload]
     result = fn(args, world, rank, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -265,6 +265,65 @@ ogbx_status ogbx_gc_traj_end(const int64_t* terminal_locs, int64_t num_terminals
 ogbx_status ogbx_nonzero_f32(const float* x, int64_t n, int64_t* out, int64_t* count,
                              void* stream);
 
+/* ======================================================================
+ * Powderworld (batched PowderworldEnv in 'task' mode, easy element set)
+ * Reference: ogbench/powderworld/powderworld_env.py:21-476, sim.py:15-590,
+ * registration ogbench/powderworld/__init__.py:3-8 (max_episode_steps 500).
+ * One env = one world_size^2 grid; state stays in HBM between calls.
+ * ====================================================================== */
+
+typedef struct ogbx_powder_env* ogbx_powder_t;
+
+typedef struct {
+  int32_t world_size;        /* 32 or 64 (PowderworldEnv world_size, :24) */
+  int32_t grid_size;         /* 4 (:25) */
+  int32_t brush_size;        /* 4 (:26) */
+  int32_t num_elems;         /* 2 = easy; 5/8 (medium/hard) -> OGBX_EINVAL for now */
+  int32_t max_episode_steps; /* TimeLimit (500 in the registry) */
+  int32_t pad;
+} ogbx_powder_opts;
+
+/* PowderworldEnv.__init__ (+ set_tasks, :81-282): the goal world of every task
+ * is replayed once on the device at create. */
+ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int32_t device,
+                               ogbx_powder_t* out);
+ogbx_status ogbx_powder_destroy(ogbx_powder_t env);
+ogbx_status ogbx_powder_describe(ogbx_powder_t env, int32_t* world_size, int32_t* xy_action_size,
+                                 int32_t* num_elems, int32_t* num_tasks, int32_t* tol);
+/* Goal world element ids, host uint8 [num_tasks, H, W] (cur_goal_world, :329). */
+ogbx_status ogbx_powder_goal_worlds(ogbx_powder_t env, uint8_t* out);
+
+/* PowderworldEnv.reset (:284-352) for envs with mask[e] != 0 (mask NULL = all).
+ * task_id: device int32 [N] in 1..num_tasks, NULL = random task per env.
+ * reset_action: device int32 [N,3] (elem index, x, y) of the random initial
+ * semantic action (sample_semantic_action, :446-451), NULL = Philox draws.
+ * obs, goal_obs: device uint8 [N, H, W, 6] (ob and info['goal']). */
+ogbx_status ogbx_powder_reset(ogbx_powder_t env, const int32_t* task_id, const uint8_t* mask,
+                              const int32_t* reset_action, uint8_t* obs, uint8_t* goal_obs,
+                              uint64_t seed, void* stream);
+
+/* k_steps x PowderworldEnv.step (:354-427) under TimeLimit.  action: device
+ * int32 [k_steps, N]; an action outside the stage's range takes a random one
+ * (np.random.randint, :358-377): draws[k, N] supplies those values, NULL =
+ * Philox.  Outputs per (k, env): obs uint8 [k,N,H,W,6], reward float32,
+ * terminated/truncated/success uint8.  auto_reset != 0 resets done envs in the
+ * same step (obs is then the new episode's first observation). */
+ogbx_status ogbx_powder_step(ogbx_powder_t env, const int32_t* action, int32_t k_steps,
+                             const int32_t* draws, uint8_t* obs, float* reward,
+                             uint8_t* terminated, uint8_t* truncated, uint8_t* success,
+                             int32_t auto_reset, void* stream);
+
+/* Device pointers to the state: world uint8 [N, H*W] (id | GravityInter<<5 |
+ * DidGravity<<6), ctrl int32 [N] (stage | elem<<2 | x<<8 | task<<16),
+ * elapsed int32 [N].  Writable (state restore). */
+ogbx_status ogbx_powder_state(ogbx_powder_t env, uint8_t** world, int32_t** ctrl,
+                              int32_t** elapsed);
+
+/* `steps` x PWSim.forward (sim.py:363-380) on packed worlds, device uint8
+ * [n_worlds, H*W] in -> out (may alias). */
+ogbx_status ogbx_powder_forward(ogbx_powder_t env, const uint8_t* world_in, int64_t n_worlds,
+                                int32_t steps, uint8_t* world_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

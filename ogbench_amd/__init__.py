@@ -11,6 +11,7 @@ All compute runs in libogbx.so (HIP, gfx950); there is no CPU fallback.
 """
 
 from .locomaze import MazeEnv, parse_env_id
+from .powderworld import PowderworldEnv
 from .registry import make, registered_env_ids
 
-__all__ = ['MazeEnv', 'make', 'parse_env_id', 'registered_env_ids']
+__all__ = ['MazeEnv', 'PowderworldEnv', 'make', 'parse_env_id', 'registered_env_ids']

@@ -43,6 +43,17 @@ class MazeOpts(ctypes.Structure):
     ]
 
 
+class PowderOpts(ctypes.Structure):
+    _fields_ = [
+        ('world_size', c_int32),
+        ('grid_size', c_int32),
+        ('brush_size', c_int32),
+        ('num_elems', c_int32),
+        ('max_episode_steps', c_int32),
+        ('pad', c_int32),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGNATURES = {
     'ogbx_last_error': (c_char_p, []),
@@ -70,6 +81,19 @@ _SIGNATURES = {
     'ogbx_maze_xy_to_ij': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     'ogbx_maze_ij_to_xy': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     'ogbx_maze_oracle_subgoal': (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    # powderworld
+    'ogbx_powder_create': (c_int32, [P(PowderOpts), c_int64, c_int32, P(c_void_p)]),
+    'ogbx_powder_destroy': (c_int32, [c_void_p]),
+    'ogbx_powder_describe': (c_int32, [c_void_p, P(c_int32), P(c_int32), P(c_int32), P(c_int32), P(c_int32)]),
+    'ogbx_powder_goal_worlds': (c_int32, [c_void_p, c_void_p]),
+    'ogbx_powder_reset': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    'ogbx_powder_step': (
+        c_int32,
+        [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+         c_void_p],
+    ),
+    'ogbx_powder_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p)]),
+    'ogbx_powder_forward': (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
 }
 
 _lock = threading.Lock()
