@@ -139,9 +139,12 @@ ogbx_status ogbx_maze_step(ogbx_maze_t env, const void* action, int32_t action_i
                            int32_t auto_reset, void* stream);
 
 /* Device pointers of the env-owned state (for checkpoint/restore and tests):
- * qpos f64[N,2], goal_xy f64[N,2], elapsed i32[N], task_id i32[N]. */
+ * qpos f64[N,2], goal_xy f64[N,2], elapsed i32[N], task_id i32[N],
+ * episode u32[N] (per-env reset counter = the Philox counter word of that
+ * env's reset draws; zeroing it re-seeds the env: reset(seed=s) twice gives
+ * the same episode, as gymnasium's reseeding does). */
 ogbx_status ogbx_maze_state(ogbx_maze_t env, double** qpos, double** goal_xy, int32_t** elapsed,
-                            int32_t** task_id);
+                            int32_t** task_id, uint32_t** episode);
 
 /* Free-standing physics: advance `n` point masses one PointEnv step without
  * any env bookkeeping: qpos_out = mj_step^5(qpos + 0.2*action).  Used by the
@@ -315,9 +318,10 @@ ogbx_status ogbx_powder_step(ogbx_powder_t env, const int32_t* action, int32_t k
 
 /* Device pointers to the state: world uint8 [N, H*W] (id | GravityInter<<5 |
  * DidGravity<<6), ctrl int32 [N] (stage | elem<<2 | x<<8 | task<<16),
- * elapsed int32 [N].  Writable (state restore). */
+ * elapsed int32 [N], episode uint32 [N] (Philox counter word, as for
+ * ogbx_maze_state).  Writable (state restore). */
 ogbx_status ogbx_powder_state(ogbx_powder_t env, uint8_t** world, int32_t** ctrl,
-                              int32_t** elapsed);
+                              int32_t** elapsed, uint32_t** episode);
 
 /* `steps` x PWSim.forward (sim.py:363-380) on packed worlds, device uint8
  * [n_worlds, H*W] in -> out (may alias). */

@@ -744,12 +744,13 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
 }
 
 ogbx_status ogbx_maze_state(ogbx_maze_t e, double** qpos, double** goal_xy, int32_t** elapsed,
-                            int32_t** task_id) {
+                            int32_t** task_id, uint32_t** episode) {
   OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
   if (qpos) *qpos = e->S.qpos;
   if (goal_xy) *goal_xy = e->S.goal;
   if (elapsed) *elapsed = e->S.elapsed;
   if (task_id) *task_id = e->S.task;
+  if (episode) *episode = e->S.episode;
   // A restore through these pointers counts as a reset.
   e->was_reset = true;
   return OGBX_OK;

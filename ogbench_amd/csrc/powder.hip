@@ -15,12 +15,18 @@
 // Layout in HBM: world u8[N, H*W], one byte per cell = element id (bits 0-4)
 // | GravityInter (bit 5, channel 2) | DidGravity (bit 6, channel 8); every
 // other channel of the reference's (9,H,W) float32 world is 0 or a function of
-// the id for easy worlds.  ctrl i32[N] = stage | elem<<2 | x<<8 | task<<16,
-// elapsed i32[N], episode u32[N].  Obs u8[N, H, W, 6].
+// the id for easy worlds.  ctrl i32[N] = stage | elem<<2 | x<<8 | task<<16 |
+// success<<24 (success of the current world, cached: the world only changes
+// on the third step of an action and on resets), elapsed i32[N], episode
+// u32[N].  Obs u8[N, H, W, 6].
 //
-// One 256-thread workgroup per env; the world lives in LDS for the whole
-// launch (k_steps steps); each thread owns a contiguous run of CPT cells of
-// one row (CPT = H*W/256: 16 at 64x64, 4 at 32x32).
+// Kernel shape: one 256-thread workgroup per env.  Thread t owns CPT = H*W/256
+// consecutive cells of one row (16 at 64x64, 4 at 32x32), held in registers as
+// packed bytes ("segment").  Neighbour rows are exchanged through an LDS copy
+// of the world; a forward pass (stone rule + gravity, whose row coupling spans
+// r-2..r+1) costs two barriers.  Observations are staged in LDS and leave as
+// fully coalesced 16-byte stores (the obs write, 24 KB per 64x64 env-step, is
+// the HBM floor of the path).
 #include <array>
 #include <cstring>
 #include <string>
@@ -30,19 +36,40 @@
 
 namespace ogbx {
 
-constexpr int kPwMaxCells = 64 * 64;
 constexpr int kPwMaxSeq = 256;
 constexpr int kPwMaxTasks = 8;
-constexpr uint8_t kIdMask = 31, kGrav = 32, kDidg = 64;
+constexpr uint32_t kIdMask = 31u, kGrav = 32u, kDidg = 64u;
+constexpr int kCtrlSuccess = 1 << 24;
 
 // density (channel 1) and default GravityInter (channel 2) per id: sim.py:15-37
-__constant__ uint8_t c_density[21] = {1, 4, 3, 2, 0, 4, 4, 0, 4, 3, 3, 2, 2, 4, 2, 4, 3, 3, 3, 4, 3};
-__constant__ uint8_t c_gravity[21] = {1, 0, 1, 1, 1, 0, 0, 1, 0, 1, 1, 1, 1, 0, 1, 0, 1, 1, 1, 0, 1};
+constexpr uint8_t kDensity[21] = {1, 4, 3, 2, 0, 4, 4, 0, 4, 3, 3, 2, 2, 4, 2, 4, 3, 3, 3, 4, 3};
+constexpr uint8_t kGravity[21] = {1, 0, 1, 1, 1, 0, 0, 1, 0, 1, 1, 1, 1, 0, 1, 0, 1, 1, 1, 0, 1};
+constexpr uint64_t pack_density() {
+  uint64_t v = 0;
+  for (int i = 0; i < 21; ++i) v |= (uint64_t)kDensity[i] << (3 * i);
+  return v;
+}
+constexpr uint32_t pack_gravity() {
+  uint32_t v = 0;
+  for (int i = 0; i < 21; ++i) v |= (uint32_t)kGravity[i] << i;
+  return v;
+}
+constexpr uint64_t kDensPacked = pack_density();  // 3 bits per id
+constexpr uint32_t kGravPacked = pack_gravity();  // 1 bit per id
+
+__device__ __forceinline__ uint32_t dens_of(uint32_t v) {
+  return (uint32_t)(kDensPacked >> (3u * (v & kIdMask))) & 7u;
+}
+__device__ __forceinline__ uint32_t elem_cell(uint32_t id) {
+  return id | (((kGravPacked >> id) & 1u) << 5);
+}
+// BehaviorGravity's did-gravity reset (sim.py:477): cleared where gravity == 1.
+__device__ __forceinline__ uint32_t rd(uint32_t v) { return (v & kGrav) ? (v & ~kDidg) : v; }
 
 struct PowderParams {
   int32_t H, W, grid, brush, xy_size, num_elems, num_tasks, max_steps, tol;
   int32_t elem_ids[8];           // _elems: element id per element index
-  uint8_t lut[21][4];            // render colour of each id (uint8(color*255))
+  uint32_t lut[32];              // render colour of each id, R | G<<8 | B<<16
   int32_t seq_len[kPwMaxTasks];  // goal replay sequences (elem idx, x, y)
   int8_t seq[kPwMaxTasks][kPwMaxSeq][3];
 };
@@ -54,175 +81,225 @@ struct PowderState {
   uint32_t* episode;
 };
 
-__device__ inline uint8_t elem_cell(int id) {
-  return (uint8_t)(id | (c_gravity[id] ? kGrav : 0));
-}
+template <int WS>
+struct Geo {
+  static constexpr int H = WS, W = WS, CELLS = WS * WS, CPT = CELLS / 256, NW = CPT / 4;
+  static constexpr int TPR = W / CPT, OBS = CELLS * 6;
+  static_assert(CPT % 4 == 0 && W % CPT == 0, "segment must be whole words of one row");
+};
 
-// ---- block-level pieces (all 256 threads of the env's workgroup call them)
+// A thread's CPT cells as packed bytes (NW 32-bit words).
+template <int NW>
+struct Seg {
+  uint32_t w[NW];
+  __device__ __forceinline__ uint32_t get(int k) const { return (w[k >> 2] >> ((k & 3) * 8)) & 0xffu; }
+  __device__ __forceinline__ void set(int k, uint32_t v) {
+    const int s = (k & 3) * 8;
+    w[k >> 2] = (w[k >> 2] & ~(0xffu << s)) | ((v & 0xffu) << s);
+  }
+};
 
-// One PWSim.forward for an easy world in LDS (a -> a, scratch b/f).
-__device__ void pw_forward(uint8_t* a, uint8_t* b, uint8_t* f, int H, int W, int cpt) {
-  const int t = threadIdx.x;
-  const int r = (t * cpt) / W, c0 = (t * cpt) % W;
-  // BehaviorStone (sim.py:580-590): stone.grav = stone(r-1,c-1)+stone(r-1,c+1) < 2
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    uint8_t v = a[r * W + c];
-    if ((v & kIdMask) == 9) {
-      int sup = 0;
-      if (r > 0) {
-        if (c > 0 && (a[(r - 1) * W + c - 1] & kIdMask) == 9) ++sup;
-        if (c < W - 1 && (a[(r - 1) * W + c + 1] & kIdMask) == 9) ++sup;
-      }
-      v = (uint8_t)((v & ~kGrav) | (sup < 2 ? kGrav : 0));
-    }
-    b[r * W + c] = v;
-  }
-  __syncthreads();
-  // BehaviorGravity (sim.py:476-501): did-gravity reset where gravity == 1, then
-  // swap with the cell below (periodic roll) when it is lighter and both have
-  // gravity; a cell that both sinks and receives keeps its content.
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    uint8_t v = b[r * W + c];
-    if (v & kGrav) v &= (uint8_t)~kDidg;
-    const int rb = r + 1 == H ? 0 : r + 1;
-    const uint8_t w = b[rb * W + c];
-    const bool dbb = (int)c_density[w & kIdMask] - (int)c_density[v & kIdMask] < 0 && (v & kGrav) &&
-                     (w & kGrav);
-    b[r * W + c] = v;  // did-gravity reset applied in place (own cell only)
-    f[r * W + c] = dbb;
-  }
-  __syncthreads();
-  uint8_t real[64];
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    const int ra = r == 0 ? H - 1 : r - 1;
-    real[k] = f[r * W + c] && !f[ra * W + c];
-  }
-  __syncthreads();
-  for (int k = 0; k < cpt; ++k) f[r * W + c0 + k] = real[k];
-  __syncthreads();
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    const int ra = r == 0 ? H - 1 : r - 1, rb = r + 1 == H ? 0 : r + 1;
-    auto reset_didg = [](uint8_t v) { return (v & kGrav) ? (uint8_t)(v & ~kDidg) : v; };
-    uint8_t v;
-    if (f[r * W + c]) {
-      v = reset_didg(b[rb * W + c]);
-    } else if (f[ra * W + c]) {
-      v = (uint8_t)(reset_didg(b[ra * W + c]) | kDidg);
-    } else {
-      v = b[r * W + c];
-    }
-    a[r * W + c] = v;
-  }
-  __syncthreads();
-}
-
-// Brush paint (powderworld_env.py:380-391): elem over the brush square unless wall.
-__device__ void pw_paint(uint8_t* a, int W, int cpt, int elem_id, int rx, int ry, int brush) {
-  const int t = threadIdx.x;
-  const int r = (t * cpt) / W, c0 = (t * cpt) % W;
-  if (r >= ry && r < ry + brush) {
-    for (int k = 0; k < cpt; ++k) {
-      const int c = c0 + k;
-      if (c >= rx && c < rx + brush && (a[r * W + c] & kIdMask) != 1) a[r * W + c] = elem_cell(elem_id);
-    }
-  }
-  __syncthreads();
-}
-
-// Observation (powderworld_env.py:462-476): RGB of the world + action frame.
-__device__ void pw_observe(const PowderParams& P, const uint8_t* a, uint8_t* obs, int stage,
-                           int elem_id, int x) {
-  const int W = P.W, cpt = (P.H * P.W) >> 8;
-  const int t = threadIdx.x;
-  const int r = (t * cpt) / W, c0 = (t * cpt) % W;
-  const int rx = x * P.grid;
-  uint8_t buf[16 * 6];
-  const int nout = cpt * 6;
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    const int id = a[r * W + c] & kIdMask;
-    buf[6 * k + 0] = P.lut[id][0];
-    buf[6 * k + 1] = P.lut[id][1];
-    buf[6 * k + 2] = P.lut[id][2];
-    const bool act = stage == 1 || (stage == 2 && c >= rx && c < rx + P.brush);
-    buf[6 * k + 3] = act ? P.lut[elem_id][0] : 0;
-    buf[6 * k + 4] = act ? P.lut[elem_id][1] : 0;
-    buf[6 * k + 5] = act ? P.lut[elem_id][2] : 0;
-  }
-  uint8_t* dst = obs + (size_t)(t * cpt) * 6;
-  if ((nout & 15) == 0) {
-    for (int q = 0; q < nout; q += 16) {
-      uint4 v;
-      memcpy(&v, buf + q, 16);
-      *reinterpret_cast<uint4*>(dst + q) = v;
-    }
+template <int NW>
+__device__ __forceinline__ Seg<NW> load_seg(const uint8_t* p) {
+  Seg<NW> s;
+  if constexpr (NW == 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    s.w[0] = v.x, s.w[1] = v.y, s.w[2] = v.z, s.w[3] = v.w;
+  } else if constexpr (NW == 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    s.w[0] = v.x, s.w[1] = v.y;
   } else {
-    for (int q = 0; q < nout; q += 8) {
-      uint2 v;
-      memcpy(&v, buf + q, 8);
-      *reinterpret_cast<uint2*>(dst + q) = v;
+    s.w[0] = *reinterpret_cast<const uint32_t*>(p);
+  }
+  return s;
+}
+
+template <int NW>
+__device__ __forceinline__ void store_seg(uint8_t* p, const Seg<NW>& s) {
+  if constexpr (NW == 4) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(s.w[0], s.w[1], s.w[2], s.w[3]);
+  } else if constexpr (NW == 2) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(s.w[0], s.w[1]);
+  } else {
+    *reinterpret_cast<uint32_t*>(p) = s.w[0];
+  }
+}
+
+template <int WS>
+struct alignas(16) PwShared {
+  alignas(16) uint8_t a[WS * WS];  // world mirror (neighbour exchange)
+  alignas(16) uint8_t f[WS * WS];  // gravity "moves down" flags
+  alignas(16) uint32_t ob[WS * WS * 6 / 4];  // observation staging
+  uint32_t lut[32];
+  int32_t elem_ids[8];
+  int32_t red[4];
+};
+
+// Per-thread view of the env's workgroup.
+template <int WS>
+struct Blk {
+  using G = Geo<WS>;
+  using S = Seg<G::NW>;
+  PwShared<WS>& sh;
+  int t, r, c0;
+  __device__ __forceinline__ explicit Blk(PwShared<WS>& s)
+      : sh(s), t((int)threadIdx.x), r((int)threadIdx.x / G::TPR), c0(((int)threadIdx.x % G::TPR) * G::CPT) {}
+
+  __device__ __forceinline__ const uint8_t* row(const uint8_t* base, int R) const { return base + R * G::W + c0; }
+
+  // BehaviorStone (sim.py:580-590) for one row segment: a stone keeps gravity
+  // unless both up-left and up-right neighbours are stone (zero-padded conv).
+  __device__ __forceinline__ S stone(S cur, const S& up, uint32_t upL, uint32_t upR, bool has_up) const {
+#pragma unroll
+    for (int k = 0; k < G::CPT; ++k) {
+      const uint32_t v = cur.get(k);
+      const uint32_t ul = k == 0 ? upL : up.get(k - 1);
+      const uint32_t ur = k == G::CPT - 1 ? upR : up.get(k + 1);
+      const bool both = has_up && (ul & kIdMask) == 9u && (ur & kIdMask) == 9u;
+      if ((v & kIdMask) == 9u) cur.set(k, (v & ~kGrav) | (both ? 0u : kGrav));
     }
+    return cur;
   }
-}
 
-// Goal mismatch count (powderworld_env.py:410-418): a goal cell matches if the
-// world id equals it at the cell or one of the 4 periodic neighbours.
-__device__ int pw_errors(const PowderParams& P, const uint8_t* a, const uint8_t* goal, int* red) {
-  const int H = P.H, W = P.W, cpt = (H * W) >> 8;
+  __device__ __forceinline__ uint32_t left_byte(const uint8_t* base, int R) const {
+    return c0 > 0 ? base[R * G::W + c0 - 1] : 0u;
+  }
+  __device__ __forceinline__ uint32_t right_byte(const uint8_t* base, int R) const {
+    return c0 + G::CPT < G::W ? base[R * G::W + c0 + G::CPT] : 0u;
+  }
+
+  // One PWSim.forward (stone rule, then gravity with periodic rolls) followed
+  // by the brush paint (powderworld_env.py:380-391), own = this thread's
+  // segment; LDS `a` must mirror the world on entry and mirrors it on exit.
+  // paint_id < 0: no paint.
+  __device__ __forceinline__ void forward_paint(S& own, int paint_id, int rx, int ry, int brush) const {
+    constexpr int H = G::H;
+    const uint8_t* A = sh.a;
+    const int rm1 = r == 0 ? H - 1 : r - 1, rm2 = r < 2 ? r + H - 2 : r - 2, rp1 = r + 1 == H ? 0 : r + 1;
+    const S a_m2 = load_seg<G::NW>(row(A, rm2));
+    const S a_m1 = load_seg<G::NW>(row(A, rm1));
+    const S a_p1 = load_seg<G::NW>(row(A, rp1));
+    const S b_m1 = stone(a_m1, a_m2, left_byte(A, rm2), right_byte(A, rm2), rm1 > 0);
+    const S b_0 = stone(own, a_m1, left_byte(A, rm1), right_byte(A, rm1), r > 0);
+    const S b_p1 = stone(a_p1, own, left_byte(A, r), right_byte(A, r), rp1 > 0);
+    // BehaviorGravity (sim.py:476-501): a cell moves down when the cell below
+    // is lighter and both have gravity
+    S dbb;
+#pragma unroll
+    for (int k = 0; k < G::NW; ++k) dbb.w[k] = 0;
+#pragma unroll
+    for (int k = 0; k < G::CPT; ++k) {
+      const uint32_t v = b_0.get(k), w = b_p1.get(k);
+      const bool m = dens_of(w) < dens_of(v) && (v & kGrav) && (w & kGrav);
+      if (m) dbb.w[k >> 2] |= 1u << ((k & 3) * 8);
+    }
+    store_seg(sh.f + r * G::W + c0, dbb);
+    __syncthreads();
+    const S f_m1 = load_seg<G::NW>(row(sh.f, rm1));
+    const S f_m2 = load_seg<G::NW>(row(sh.f, rm2));
+    const bool in_rows = paint_id >= 0 && r >= ry && r < ry + brush;
+    const uint32_t pcell = paint_id >= 0 ? elem_cell((uint32_t)paint_id) : 0u;
+#pragma unroll
+    for (int k = 0; k < G::CPT; ++k) {
+      // overlap resolution (sim.py:487-489): a cell that sinks onto a sinking
+      // cell stays; real moves are dbb & ~dbb(above)
+      const bool real0 = dbb.get(k) && !f_m1.get(k);
+      const bool realm1 = f_m1.get(k) && !f_m2.get(k);
+      uint32_t v = real0 ? rd(b_p1.get(k)) : (realm1 ? (rd(b_m1.get(k)) | kDidg) : rd(b_0.get(k)));
+      const int c = c0 + k;
+      if (in_rows && c >= rx && c < rx + brush && (v & kIdMask) != 1u) v = pcell;
+      own.set(k, v);
+    }
+    store_seg(sh.a + r * G::W + c0, own);
+    __syncthreads();
+  }
+
+  // Goal mismatch count (powderworld_env.py:410-418): a goal cell matches if
+  // the world id equals it at the cell or at one of its 4 periodic
+  // neighbours.  LDS `a` must mirror the world.  Returns the block total.
+  __device__ __forceinline__ int errors(const S& own, const uint8_t* __restrict__ goal) const {
+    constexpr int H = G::H, W = G::W;
+    const uint8_t* A = sh.a;
+    const int rm1 = r == 0 ? H - 1 : r - 1, rp1 = r + 1 == H ? 0 : r + 1;
+    const S up = load_seg<G::NW>(row(A, rm1));
+    const S dn = load_seg<G::NW>(row(A, rp1));
+    const S g = load_seg<G::NW>(goal + r * W + c0);
+    const uint32_t lft = A[r * W + (c0 == 0 ? W - 1 : c0 - 1)];
+    const uint32_t rgt = A[r * W + (c0 + G::CPT == W ? 0 : c0 + G::CPT)];
+    int err = 0;
+#pragma unroll
+    for (int k = 0; k < G::CPT; ++k) {
+      const uint32_t gk = g.get(k);
+      const uint32_t l = k == 0 ? lft : own.get(k - 1);
+      const uint32_t rr = k == G::CPT - 1 ? rgt : own.get(k + 1);
+      const bool m = (own.get(k) & kIdMask) == gk || (l & kIdMask) == gk || (rr & kIdMask) == gk ||
+                     (up.get(k) & kIdMask) == gk || (dn.get(k) & kIdMask) == gk;
+      err += m ? 0 : 1;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
+    if ((t & 63) == 0) sh.red[t >> 6] = err;
+    __syncthreads();
+    const int total = sh.red[0] + sh.red[1] + sh.red[2] + sh.red[3];
+    return total;
+  }
+
+  // Blank world (border walls, sim.py np_to_pw of zeros) + one brush paint.
+  // The reference runs PWSim.forward on the blank world before the paint; it
+  // is an identity there (nothing has a lighter cell below, no stone).
+  __device__ __forceinline__ S reset_world(int paint_id, int rx, int ry, int brush) const {
+    S own;
+#pragma unroll
+    for (int k = 0; k < G::CPT; ++k) {
+      const int c = c0 + k;
+      const bool border = r == 0 || r == G::H - 1 || c == 0 || c == G::W - 1;
+      uint32_t v = border ? elem_cell(1) : elem_cell(0);
+      if (r >= ry && r < ry + brush && c >= rx && c < rx + brush && !border) v = elem_cell((uint32_t)paint_id);
+      own.set(k, v);
+    }
+    return own;
+  }
+
+  // Observation (powderworld_env.py:462-476): RGB of the world + action frame
+  // (stage 1: whole frame in the element colour; stage 2: columns of x).
+  // Staged in LDS, then written as coalesced 16-byte stores.
+  __device__ __forceinline__ void observe(const S& own, uint8_t* __restrict__ dst, int stage, uint32_t acol,
+                                          int rx, int brush) const {
+    __syncthreads();  // staging buffer free (previous copy-out done)
+    uint32_t words[G::CPT * 6 / 4];
+#pragma unroll
+    for (int p = 0; p < G::CPT / 2; ++p) {
+      const int k0 = 2 * p, k1 = 2 * p + 1;
+      const uint32_t C0 = sh.lut[own.get(k0) & kIdMask], C1 = sh.lut[own.get(k1) & kIdMask];
+      const bool f0 = stage == 1 || (stage == 2 && c0 + k0 >= rx && c0 + k0 < rx + brush);
+      const bool f1 = stage == 1 || (stage == 2 && c0 + k1 >= rx && c0 + k1 < rx + brush);
+      const uint32_t A0 = f0 ? acol : 0u, A1 = f1 ? acol : 0u;
+      words[3 * p + 0] = C0 | (A0 << 24);
+      words[3 * p + 1] = (A0 >> 8) | (C1 << 16);
+      words[3 * p + 2] = ((C1 >> 16) & 0xffu) | (A1 << 8);
+    }
+    uint32_t* st = sh.ob + t * (G::CPT * 6 / 4);
+    if constexpr ((G::CPT * 6 / 4) % 4 == 0) {
+#pragma unroll
+      for (int q = 0; q < G::CPT * 6 / 4; q += 4)
+        *reinterpret_cast<uint4*>(st + q) = make_uint4(words[q], words[q + 1], words[q + 2], words[q + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < G::CPT * 6 / 4; q += 2) *reinterpret_cast<uint2*>(st + q) = make_uint2(words[q], words[q + 1]);
+    }
+    __syncthreads();
+    const uint4* src = reinterpret_cast<const uint4*>(sh.ob);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int q = t; q < G::OBS / 16; q += 256) d[q] = src[q];
+  }
+};
+
+template <int WS>
+__device__ __forceinline__ void load_tables(PwShared<WS>& sh, const PowderParams* __restrict__ Pp) {
   const int t = threadIdx.x;
-  const int r = (t * cpt) / W, c0 = (t * cpt) % W;
-  int err = 0;
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    const int g = goal[r * W + c];
-    const int cl = c == 0 ? W - 1 : c - 1, cr = c + 1 == W ? 0 : c + 1;
-    const int ra = r == 0 ? H - 1 : r - 1, rb = r + 1 == H ? 0 : r + 1;
-    const bool m = (a[r * W + c] & kIdMask) == g || (a[r * W + cl] & kIdMask) == g ||
-                   (a[r * W + cr] & kIdMask) == g || (a[ra * W + c] & kIdMask) == g ||
-                   (a[rb * W + c] & kIdMask) == g;
-    err += !m;
-  }
-  // wave reduction, then one LDS add per wave
-  for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
-  if (threadIdx.x == 0) *red = 0;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) atomicAdd(red, err);
-  __syncthreads();
-  const int total = *red;
-  __syncthreads();
-  return total;
-}
-
-// Blank world (border walls) + one random semantic action x3 steps
-// (powderworld_env.py:307-341): forward is an identity on the blank world.
-__device__ void pw_reset_world(const PowderParams& P, uint8_t* a, uint8_t* b, uint8_t* f, int elem,
-                               int x, int y) {
-  const int H = P.H, W = P.W, cpt = (H * W) >> 8;
-  const int t = threadIdx.x;
-  const int r = (t * cpt) / W, c0 = (t * cpt) % W;
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    const bool border = r == 0 || r == H - 1 || c == 0 || c == W - 1;
-    a[r * W + c] = border ? elem_cell(1) : elem_cell(0);
-  }
-  __syncthreads();
-  pw_forward(a, b, f, H, W, cpt);
-  pw_paint(a, W, cpt, P.elem_ids[elem], x * P.grid, y * P.grid, P.brush);
-}
-
-__device__ inline void load_world(uint8_t* a, const uint8_t* src, int n) {
-  for (int q = threadIdx.x * 16; q < n; q += blockDim.x * 16)
-    *reinterpret_cast<uint4*>(a + q) = *reinterpret_cast<const uint4*>(src + q);
-  __syncthreads();
-}
-
-__device__ inline void store_world(uint8_t* dst, const uint8_t* a, int n) {
-  for (int q = threadIdx.x * 16; q < n; q += blockDim.x * 16)
-    *reinterpret_cast<uint4*>(dst + q) = *reinterpret_cast<const uint4*>(a + q);
+  if (t < 32) sh.lut[t] = Pp->lut[t];
+  if (t < 8) sh.elem_ids[t] = Pp->elem_ids[t];
 }
 
 __device__ inline uint32_t pw_draw(uint64_t env, uint32_t ep, uint32_t slot, uint32_t k0, uint32_t k1,
@@ -233,61 +310,68 @@ __device__ inline uint32_t pw_draw(uint64_t env, uint32_t ep, uint32_t slot, uin
 
 // ---------------------------------------------------------------- kernels
 
-__global__ void __launch_bounds__(256) pw_goal_kernel(const PowderParams* __restrict__ Pp,
-                                                      uint8_t* goals) {
-  const PowderParams& P = *Pp;
-  __shared__ uint8_t a[kPwMaxCells], b[kPwMaxCells], f[kPwMaxCells];
+// Goal worlds: replay each task's semantic action sequence (one forward +
+// paint per action) from the blank world (powderworld_env.py:322-329).
+template <int WS>
+__global__ void __launch_bounds__(256) pw_goal_kernel(const PowderParams* __restrict__ Pp, uint8_t* goals) {
+  __shared__ PwShared<WS> sh;
+  Blk<WS> b(sh);
+  using G = Geo<WS>;
+  load_tables(sh, Pp);
   const int task = blockIdx.x;
-  const int H = P.H, W = P.W, cpt = (H * W) >> 8;
-  const int t = threadIdx.x;
-  const int r = (t * cpt) / W, c0 = (t * cpt) % W;
-  for (int k = 0; k < cpt; ++k) {
-    const int c = c0 + k;
-    const bool border = r == 0 || r == H - 1 || c == 0 || c == W - 1;
-    a[r * W + c] = border ? elem_cell(1) : elem_cell(0);
-  }
+  const int grid = Pp->grid, brush = Pp->brush, len = Pp->seq_len[task];
+  typename Blk<WS>::S own = b.reset_world(0, -1000, -1000, brush);
+  store_seg(sh.a + b.r * G::W + b.c0, own);
   __syncthreads();
-  for (int s = 0; s < P.seq_len[task]; ++s) {
-    pw_forward(a, b, f, H, W, cpt);
-    pw_paint(a, W, cpt, P.elem_ids[P.seq[task][s][0]], P.seq[task][s][1] * P.grid,
-             P.seq[task][s][2] * P.grid, P.brush);
+  for (int s = 0; s < len; ++s) {
+    const int8_t* q = Pp->seq[task][s];
+    b.forward_paint(own, sh.elem_ids[q[0]], q[1] * grid, q[2] * grid, brush);
   }
-  for (int k = 0; k < cpt; ++k) goals[(size_t)task * H * W + r * W + c0 + k] = a[r * W + c0 + k] & kIdMask;
+  typename Blk<WS>::S ids;
+#pragma unroll
+  for (int k = 0; k < G::CPT; ++k) ids.set(k, own.get(k) & kIdMask);
+  store_seg(goals + (size_t)task * G::CELLS + b.r * G::W + b.c0, ids);
 }
 
-__global__ void __launch_bounds__(256) pw_reset_kernel(const PowderParams* __restrict__ Pp,
-                                                       PowderState S, const uint8_t* goals,
-                                                       const int32_t* task_id, const uint8_t* mask,
-                                                       const int32_t* reset_action, uint8_t* obs,
-                                                       uint8_t* goal_obs, uint32_t k0, uint32_t k1) {
-  const PowderParams& P = *Pp;
-  __shared__ uint8_t a[kPwMaxCells], b[kPwMaxCells], f[kPwMaxCells];
+template <int WS>
+__global__ void __launch_bounds__(256) pw_reset_kernel(const PowderParams* __restrict__ Pp, PowderState S,
+                                                       const uint8_t* __restrict__ goals,
+                                                       const int32_t* __restrict__ task_id,
+                                                       const uint8_t* __restrict__ mask,
+                                                       const int32_t* __restrict__ reset_action,
+                                                       uint8_t* __restrict__ obs, uint8_t* __restrict__ goal_obs,
+                                                       uint32_t k0, uint32_t k1) {
+  using G = Geo<WS>;
+  __shared__ PwShared<WS> sh;
   const int64_t e = blockIdx.x;
   if (mask != nullptr && mask[e] == 0) return;
-  const int HW = P.H * P.W;
+  Blk<WS> b(sh);
+  load_tables(sh, Pp);
+  const int grid = Pp->grid, brush = Pp->brush, ne = Pp->num_elems, xy = Pp->xy_size, nt = Pp->num_tasks;
   const uint32_t ep = S.episode[e] + 1u;
-  int task = task_id ? task_id[e] : 1 + (int)pw_draw(e, ep, 0, k0, k1, (uint32_t)P.num_tasks);
-  if (task < 1 || task > P.num_tasks) task = 1;
+  int task = task_id ? task_id[e] : 1 + (int)pw_draw(e, ep, 0, k0, k1, (uint32_t)nt);
+  if (task < 1 || task > nt) task = 1;
   int elem, x, y;
   if (reset_action) {
-    elem = reset_action[3 * e];
-    x = reset_action[3 * e + 1];
-    y = reset_action[3 * e + 2];
+    elem = reset_action[3 * e], x = reset_action[3 * e + 1], y = reset_action[3 * e + 2];
   } else {
-    elem = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)P.num_elems);
-    x = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)P.xy_size);
-    y = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)P.xy_size);
+    elem = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
+    x = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
+    y = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
   }
-  pw_reset_world(P, a, b, f, elem, x, y);
-  store_world(S.world + (size_t)e * HW, a, HW);
-  pw_observe(P, a, obs + (size_t)e * HW * 6, 0, 0, 0);
-  // goal observation: render of the goal world (stage 0 -> empty action frame)
-  const uint8_t* g = goals + (size_t)(task - 1) * HW;
-  for (int q = threadIdx.x; q < HW; q += blockDim.x) b[q] = g[q];
+  __syncthreads();  // tables
+  typename Blk<WS>::S own = b.reset_world(sh.elem_ids[elem], x * grid, y * grid, brush);
+  store_seg(sh.a + b.r * G::W + b.c0, own);
+  store_seg(S.world + (size_t)e * G::CELLS + b.r * G::W + b.c0, own);
   __syncthreads();
-  pw_observe(P, b, goal_obs + (size_t)e * HW * 6, 0, 0, 0);
+  const uint8_t* goal = goals + (size_t)(task - 1) * G::CELLS;
+  const int errs = b.errors(own, goal);
+  b.observe(own, obs + (size_t)e * G::OBS, 0, 0u, 0, brush);
+  // goal observation: render of the goal world (stage 0 -> empty action frame)
+  const typename Blk<WS>::S g = load_seg<G::NW>(goal + b.r * G::W + b.c0);
+  b.observe(g, goal_obs + (size_t)e * G::OBS, 0, 0u, 0, brush);
   if (threadIdx.x == 0) {
-    S.ctrl[e] = task << 16;
+    S.ctrl[e] = (task << 16) | (errs < Pp->tol ? kCtrlSuccess : 0);
     S.elapsed[e] = 0;
     S.episode[e] = ep;
   }
@@ -295,67 +379,76 @@ __global__ void __launch_bounds__(256) pw_reset_kernel(const PowderParams* __res
 
 // k_steps env steps per launch; actions [k, N] int32; draws [k, N] (values of
 // np.random.randint for invalid actions) or NULL = Philox.
+template <int WS>
 __global__ void __launch_bounds__(256) pw_step_kernel(
-    const PowderParams* __restrict__ Pp, PowderState S, const uint8_t* __restrict__ goals,
-    int64_t n, const int32_t* __restrict__ action, const int32_t* __restrict__ draws, int32_t k_steps,
+    const PowderParams* __restrict__ Pp, PowderState S, const uint8_t* __restrict__ goals, int64_t n,
+    const int32_t* __restrict__ action, const int32_t* __restrict__ draws, int32_t k_steps,
     uint8_t* __restrict__ obs, float* __restrict__ reward, uint8_t* __restrict__ terminated,
     uint8_t* __restrict__ truncated, uint8_t* __restrict__ success, int32_t auto_reset, uint32_t k0,
     uint32_t k1, uint32_t a0, uint32_t a1) {
-  const PowderParams& P = *Pp;
-  __shared__ uint8_t a[kPwMaxCells], b[kPwMaxCells], f[kPwMaxCells];
-  __shared__ int red;
+  using G = Geo<WS>;
+  __shared__ PwShared<WS> sh;
+  Blk<WS> b(sh);
   const int64_t e = blockIdx.x;
-  const int HW = P.H * P.W;
-  load_world(a, S.world + (size_t)e * HW, HW);
+  load_tables(sh, Pp);
+  const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
+  const int max_steps = Pp->max_steps, tol = Pp->tol;
+  uint8_t* wdst = S.world + (size_t)e * G::CELLS + b.r * G::W + b.c0;
+  typename Blk<WS>::S own = load_seg<G::NW>(wdst);
+  store_seg(sh.a + b.r * G::W + b.c0, own);
   int ctrl = S.ctrl[e];
   int el = S.elapsed[e];
   uint32_t ep = S.episode[e];
+  const uint8_t* goal = goals + (size_t)(((ctrl >> 16) & 255) - 1) * G::CELLS;
   bool dirty = false;
+  __syncthreads();
   for (int k = 0; k < k_steps; ++k) {
     const int64_t o = (int64_t)k * n + e;
     const int act = action[o];
     int stage = ctrl & 3, elem = (ctrl >> 2) & 63, x = (ctrl >> 8) & 255;
-    const int task = (ctrl >> 16) & 255;
-    auto rnd = [&](uint32_t bound) -> int {
+    bool succ = (ctrl & kCtrlSuccess) != 0;
+    auto rnd = [&](int bound) -> int {
       if (draws) return draws[o];
-      return (int)pw_draw(e, ep, (uint32_t)el, a0, a1, bound);
+      return (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)bound);
     };
     if (stage == 0) {
-      elem = act >= 0 && act < P.num_elems ? act : rnd((uint32_t)P.num_elems);
+      elem = act >= 0 && act < ne ? act : rnd(ne);
     } else if (stage == 1) {
-      x = act >= 0 && act < P.xy_size ? act : rnd((uint32_t)P.xy_size);
+      x = act >= 0 && act < xy ? act : rnd(xy);
     } else {
-      const int y = act >= 0 && act < P.xy_size ? act : rnd((uint32_t)P.xy_size);
-      pw_forward(a, b, f, P.H, P.W, HW >> 8);
-      pw_paint(a, P.W, HW >> 8, P.elem_ids[elem], x * P.grid, y * P.grid, P.brush);
+      const int y = act >= 0 && act < xy ? act : rnd(xy);
+      b.forward_paint(own, sh.elem_ids[elem], x * grid, y * grid, brush);
+      succ = b.errors(own, goal) < tol;
       dirty = true;
     }
     stage = stage == 2 ? 0 : stage + 1;
-    const int errs = pw_errors(P, a, goals + (size_t)(task - 1) * HW, &red);
-    const bool succ = errs < P.tol;
     el += 1;
-    const bool trunc = el >= P.max_steps;
-    uint8_t* ob = obs + (size_t)o * HW * 6;
-    if (auto_reset && (succ || trunc)) {
-      ep += 1u;
-      const int re = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)P.num_elems);
-      const int rx = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)P.xy_size);
-      const int ry = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)P.xy_size);
-      pw_reset_world(P, a, b, f, re, rx, ry);
-      stage = 0;
-      el = 0;
-      dirty = true;
-    }
-    ctrl = stage | (elem << 2) | (x << 8) | (task << 16);
-    pw_observe(P, a, ob, stage, P.elem_ids[elem & 7], x);
+    const bool trunc = el >= max_steps;
     if (threadIdx.x == 0) {
       reward[o] = succ ? 1.0f : 0.0f;
       terminated[o] = succ;
       truncated[o] = trunc;
       success[o] = succ;
     }
+    if (auto_reset && (succ || trunc)) {
+      ep += 1u;
+      const int re = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
+      const int rx = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
+      const int ry = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+      own = b.reset_world(sh.elem_ids[re], rx * grid, ry * grid, brush);
+      __syncthreads();  // every thread is past its reads of `a`
+      store_seg(sh.a + b.r * G::W + b.c0, own);
+      __syncthreads();
+      succ = b.errors(own, goal) < tol;
+      stage = 0;
+      el = 0;
+      dirty = true;
+    }
+    ctrl = stage | (elem << 2) | (x << 8) | (ctrl & (255 << 16)) | (succ ? kCtrlSuccess : 0);
+    const uint32_t acol = sh.lut[sh.elem_ids[elem & 7] & 31];
+    b.observe(own, obs + (size_t)o * G::OBS, stage, acol, x * grid, brush);
   }
-  if (dirty) store_world(S.world + (size_t)e * HW, a, HW);
+  if (dirty) store_seg(wdst, own);
   if (threadIdx.x == 0) {
     S.ctrl[e] = ctrl;
     S.elapsed[e] = el;
@@ -364,15 +457,19 @@ __global__ void __launch_bounds__(256) pw_step_kernel(
 }
 
 // Free-standing PWSim.forward on packed worlds [n, H*W] (tests).
+template <int WS>
 __global__ void __launch_bounds__(256) pw_forward_kernel(const PowderParams* __restrict__ Pp,
                                                          const uint8_t* in, uint8_t* out,
                                                          int32_t steps) {
-  const PowderParams& P = *Pp;
-  __shared__ uint8_t a[kPwMaxCells], b[kPwMaxCells], f[kPwMaxCells];
-  const int HW = P.H * P.W;
-  load_world(a, in + (size_t)blockIdx.x * HW, HW);
-  for (int s = 0; s < steps; ++s) pw_forward(a, b, f, P.H, P.W, HW >> 8);
-  store_world(out + (size_t)blockIdx.x * HW, a, HW);
+  using G = Geo<WS>;
+  __shared__ PwShared<WS> sh;
+  Blk<WS> b(sh);
+  const size_t off = (size_t)blockIdx.x * G::CELLS + b.r * G::W + b.c0;
+  typename Blk<WS>::S own = load_seg<G::NW>(in + off);
+  store_seg(sh.a + b.r * G::W + b.c0, own);
+  __syncthreads();
+  for (int s = 0; s < steps; ++s) b.forward_paint(own, -1, 0, 0, 0);
+  store_seg(out + off, own);
 }
 
 // Host-side task tables (powderworld_env.py:88-149), elem indices into
@@ -463,7 +560,7 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
       float v = (float)colors[i][c] / 255.0f;
       v = (1.0f - 0.0f) * v + 0.0f * v;
       v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-      P.lut[i][c] = (uint8_t)(v * 255.0f);
+      P.lut[i] |= (uint32_t)(uint8_t)(v * 255.0f) << (8 * c);
     }
   std::vector<std::vector<std::array<int, 3>>> tasks;
   easy_tasks(tasks);
@@ -486,7 +583,10 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
   if (h == hipSuccess) h = hipMemset(e->S.elapsed, 0, n * sizeof(int32_t));
   if (h == hipSuccess) h = hipMemset(e->S.episode, 0, n * sizeof(uint32_t));
   if (h == hipSuccess) {
-    hipLaunchKernelGGL(pw_goal_kernel, dim3(P.num_tasks), dim3(256), 0, 0, e->Pd, e->goals);
+    if (ws == 64)
+      hipLaunchKernelGGL(pw_goal_kernel<64>, dim3(P.num_tasks), dim3(256), 0, 0, e->Pd, e->goals);
+    else
+      hipLaunchKernelGGL(pw_goal_kernel<32>, dim3(P.num_tasks), dim3(256), 0, 0, e->Pd, e->goals);
     h = hipGetLastError();
   }
   if (h == hipSuccess) h = hipDeviceSynchronize();
@@ -538,8 +638,12 @@ ogbx_status ogbx_powder_reset(ogbx_powder_t e, const int32_t* task_id, const uin
   e->seed = seed;
   uint32_t k0, k1;
   seed_key(seed, kTagPowderReset, &k0, &k1);
-  hipLaunchKernelGGL(pw_reset_kernel, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
-                     e->Pd, e->S, e->goals, task_id, mask, reset_action, obs, goal_obs, k0, k1);
+  if (e->P.W == 64)
+    hipLaunchKernelGGL(pw_reset_kernel<64>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
+                       e->Pd, e->S, e->goals, task_id, mask, reset_action, obs, goal_obs, k0, k1);
+  else
+    hipLaunchKernelGGL(pw_reset_kernel<32>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
+                       e->Pd, e->S, e->goals, task_id, mask, reset_action, obs, goal_obs, k0, k1);
   OGBX_LAUNCHED("pw_reset_kernel");
   e->was_reset = true;
   return OGBX_OK;
@@ -557,18 +661,25 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
   uint32_t k0, k1, a0, a1;
   seed_key(e->seed, kTagPowderReset, &k0, &k1);
   seed_key(e->seed, kTagPowderAction, &a0, &a1);
-  hipLaunchKernelGGL(pw_step_kernel, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
-                     e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs, reward, terminated,
-                     truncated, success, auto_reset, k0, k1, a0, a1);
+  if (e->P.W == 64)
+    hipLaunchKernelGGL(pw_step_kernel<64>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
+                       e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs, reward, terminated,
+                       truncated, success, auto_reset, k0, k1, a0, a1);
+  else
+    hipLaunchKernelGGL(pw_step_kernel<32>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
+                       e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs, reward, terminated,
+                       truncated, success, auto_reset, k0, k1, a0, a1);
   OGBX_LAUNCHED("pw_step_kernel");
   return OGBX_OK;
 }
 
-ogbx_status ogbx_powder_state(ogbx_powder_t e, uint8_t** world, int32_t** ctrl, int32_t** elapsed) {
+ogbx_status ogbx_powder_state(ogbx_powder_t e, uint8_t** world, int32_t** ctrl, int32_t** elapsed,
+                              uint32_t** episode) {
   OGBX_CHECK(e, OGBX_EINVAL, "null handle");
   if (world) *world = e->S.world;
   if (ctrl) *ctrl = e->S.ctrl;
   if (elapsed) *elapsed = e->S.elapsed;
+  if (episode) *episode = e->S.episode;
   e->was_reset = true;
   return OGBX_OK;
 }
@@ -579,8 +690,12 @@ ogbx_status ogbx_powder_forward(ogbx_powder_t e, const uint8_t* world_in, int64_
              "ogbx_powder_forward: bad argument");
   if (n_worlds == 0) return OGBX_OK;
   OGBX_HIP(hipSetDevice(e->device));
-  hipLaunchKernelGGL(pw_forward_kernel, dim3((uint32_t)n_worlds), dim3(256), 0,
-                     (hipStream_t)stream, e->Pd, world_in, world_out, steps);
+  if (e->P.W == 64)
+    hipLaunchKernelGGL(pw_forward_kernel<64>, dim3((uint32_t)n_worlds), dim3(256), 0,
+                       (hipStream_t)stream, e->Pd, world_in, world_out, steps);
+  else
+    hipLaunchKernelGGL(pw_forward_kernel<32>, dim3((uint32_t)n_worlds), dim3(256), 0,
+                       (hipStream_t)stream, e->Pd, world_in, world_out, steps);
   OGBX_LAUNCHED("pw_forward_kernel");
   return OGBX_OK;
 }

@@ -229,14 +229,14 @@ class MazeEnv:
         return out
 
     def _state_ptrs(self):
-        q, g, e, t = _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p()
-        _lib.check(self._L.ogbx_maze_state(self._h, q, g, e, t))
-        return q.value, g.value, e.value, t.value
+        q, g, e, t, ep = (_lib.c_void_p() for _ in range(5))
+        _lib.check(self._L.ogbx_maze_state(self._h, q, g, e, t, ep))
+        return q.value, g.value, e.value, t.value, ep.value
 
     def _state_views(self):
-        """torch views of the env-owned state (qpos, goal, elapsed, task)."""
+        """torch views of the env-owned state (qpos, goal, elapsed, task, episode)."""
         torch = _torch()
-        q, g, e, t = self._state_ptrs()
+        q, g, e, t, ep = self._state_ptrs()
         n = self.num_envs
 
         return (
@@ -244,6 +244,7 @@ class MazeEnv:
             _from_ptr(g, (n, 2), torch.float64, self.device),
             _from_ptr(e, (n,), torch.int32, self.device),
             _from_ptr(t, (n,), torch.int32, self.device),
+            _from_ptr(ep, (n,), torch.int32, self.device),  # uint32 counter, viewed as int32
         )
 
     def get_xy(self):
@@ -254,15 +255,18 @@ class MazeEnv:
         return self._state_views()[1].clone()
 
     def state_dict(self):
-        q, g, e, t = self._state_views()
-        return dict(qpos=q.clone(), goal=g.clone(), elapsed=e.clone(), task=t.clone(), seed=self._seed)
+        q, g, e, t, ep = self._state_views()
+        return dict(qpos=q.clone(), goal=g.clone(), elapsed=e.clone(), task=t.clone(), episode=ep.clone(),
+                    seed=self._seed)
 
     def load_state_dict(self, sd):
-        q, g, e, t = self._state_views()
+        q, g, e, t, ep = self._state_views()
         q.copy_(sd['qpos'])
         g.copy_(sd['goal'])
         e.copy_(sd['elapsed'])
         t.copy_(sd['task'])
+        if 'episode' in sd:
+            ep.copy_(sd['episode'])
         if sd.get('seed') is not None:
             self._seed = int(sd['seed'])
         self._has_reset = True
@@ -303,7 +307,9 @@ class MazeEnv:
         if options.get('render_goal'):
             raise NotImplementedError('render_goal needs MuJoCo rendering (out of scope)')
         if seed is not None:
+            # gymnasium reseeding: the Philox stream of every reset env restarts
             self._seed = int(seed) & ((1 << 64) - 1)
+            _zero_episodes(self._state_views()[4], mask, self.device)
         elif self._seed is None:
             self._seed = (
                 int(self._init_seed) if self._init_seed is not None else int(np.random.randint(0, 2**63 - 1))
@@ -445,6 +451,15 @@ class MazeEnv:
             )
         )
         return out, contact
+
+
+def _zero_episodes(episode, mask, device):
+    """Restart the per-env Philox reset counters (all envs, or those in mask)."""
+    if mask is None:
+        episode.zero_()
+    else:
+        m = _torch().as_tensor(mask).to(device).bool().reshape(-1)
+        episode.masked_fill_(m, 0)
 
 
 def _from_ptr(addr, shape, dtype, device):

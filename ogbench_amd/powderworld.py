@@ -25,7 +25,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from .locomaze import _from_ptr, _resolve_device, _torch
+from .locomaze import _from_ptr, _resolve_device, _torch, _zero_episodes
 from .powder_tasks import EASY_TASK_NAMES, easy_task_sequences
 from .spaces import Box, Discrete
 
@@ -141,12 +141,13 @@ class PowderworldEnv:
 
     def _state_views(self):
         torch = _torch()
-        w, c, e = _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p()
-        _lib.check(self._L.ogbx_powder_state(self._h, w, c, e))
+        w, c, e, ep = (_lib.c_void_p() for _ in range(4))
+        _lib.check(self._L.ogbx_powder_state(self._h, w, c, e, ep))
         n, H = self.num_envs, self._world_size
         return (_from_ptr(w.value, (n, H, H), torch.uint8, self.device),
                 _from_ptr(c.value, (n,), torch.int32, self.device),
-                _from_ptr(e.value, (n,), torch.int32, self.device))
+                _from_ptr(e.value, (n,), torch.int32, self.device),
+                _from_ptr(ep.value, (n,), torch.int32, self.device))
 
     def world_ids(self):
         """Element id of every cell, uint8 [N, H, W] (reference self._world[:, 0])."""
@@ -157,14 +158,16 @@ class PowderworldEnv:
         return (self._state_views()[1] >> 16) & 255
 
     def state_dict(self):
-        w, c, e = self._state_views()
-        return dict(world=w.clone(), ctrl=c.clone(), elapsed=e.clone(), seed=self._seed)
+        w, c, e, ep = self._state_views()
+        return dict(world=w.clone(), ctrl=c.clone(), elapsed=e.clone(), episode=ep.clone(), seed=self._seed)
 
     def load_state_dict(self, sd):
-        w, c, e = self._state_views()
+        w, c, e, ep = self._state_views()
         w.copy_(sd['world'])
         c.copy_(sd['ctrl'])
         e.copy_(sd['elapsed'])
+        if 'episode' in sd:
+            ep.copy_(sd['episode'])
         if sd.get('seed') is not None:
             self._seed = int(sd['seed'])
 
@@ -192,7 +195,9 @@ class PowderworldEnv:
         if 'task_info' in options:
             raise NotImplementedError('custom task_info action sequences are not supported on the device')
         if seed is not None:
+            # gymnasium reseeding: the Philox stream of every reset env restarts
             self._seed = int(seed) & ((1 << 64) - 1)
+            _zero_episodes(self._state_views()[3], mask, self.device)
         elif self._seed is None:
             self._seed = (int(self._init_seed) if self._init_seed is not None
                           else int(np.random.randint(0, 2**63 - 1)))
