@@ -85,6 +85,23 @@ def _per_launch_ms(fn, launches, dev):
     return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
 
+def _traffic(kernel, kern_ms):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/traffic.json, written by scripts/prof_summary.py from separate
+    FETCH_SIZE and WRITE_SIZE passes of this same command: bytes = (2 x FETCH_SIZE
+    + WRITE_SIZE) x 1024, the gfx950 correction of MI355X_MICROARCH.md section HBM).
+    None when no summary for this kernel is committed."""
+    path = os.path.join(ROOT, 'profiles', 'traffic.json')
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
+    if not rec:
+        return None
+    return rec.get('hbm_bytes_per_launch')
+
+
 def bench_pointmaze(args, world, rank, dev):
     import ogbench_amd
 
@@ -113,6 +130,8 @@ def bench_pointmaze(args, world, rank, dev):
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
     extra = {}
+    if args.no_extras:
+        return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
     # hipGraph replay of G steps (launch-bound inner loop captured once)
     try:
         G = 32
@@ -150,7 +169,10 @@ def bench_pointmaze(args, world, rank, dev):
     fused_bytes = (8 + 16 + 4 + 3) * n * K + (16 + 16 + 4 + 4 + 16 + 4 + 4) * n
     extra['fused_k64_kernel_ms'] = fk_ms
     extra['fused_k64_achieved_GBs'] = fused_bytes / (fk_ms * 1e-3) / 1e9
+    return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
 
+
+def _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env):
     result = dict(
         metric='env steps/sec at N=65536 parallel envs, pointmaze-large, 1/2/4/8 MI355X',
         value=value,
@@ -179,7 +201,7 @@ def bench_pointmaze(args, world, rank, dev):
             peak=HBM_PEAK_GBS,
             unit='GB/s',
             frac=achieved / HBM_PEAK_GBS,
-            traffic=None,
+            traffic=_traffic('maze_step_kernel', kern_ms),
             kernel_ms=kern_ms,
             alg_bytes_per_launch=alg_bytes,
         ),
@@ -256,10 +278,14 @@ def bench_gcsample(args, world, rank, dev):
     def fused(i):
         gc.sample(B, num_batches=NB)
 
-    fused(0)
-    reps = max(1, args.steps // 32)
-    fdt = _timed(fused, reps, world, dev)
-    fk_ms = _per_launch_ms(fused, 5, dev)
+    extra = {}
+    if not args.no_extras:
+        fused(0)
+        reps = max(1, args.steps // 32)
+        fdt = _timed(fused, reps, world, dev)
+        fk_ms = _per_launch_ms(fused, 5, dev)
+        extra = dict(fused_256x1024_samples_per_s=B * NB * reps * world / fdt, fused_256x1024_kernel_ms=fk_ms,
+                     fused_256x1024_achieved_GBs=per_sample * B * NB / (fk_ms * 1e-3) / 1e9)
     result = dict(
         metric='GCDataset.sample samples/sec, humanoidmaze-large-navigate-v0 1M-row buffer, batch 1024',
         value=value, unit='samples/s', n_gpus=world, steps=args.steps, warmup=args.warmup,
@@ -268,10 +294,9 @@ def bench_gcsample(args, world, rank, dev):
         config=dict(workload='humanoidmaze-large-navigate-v0 offline replay', rows=R, batch=B,
                     agent_config='gciql humanoid (discount 0.995)', parallelism=f'replica x{world}'),
         roofline=dict(bound='hbm', kernel='gc_sample_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=None, kernel_ms=kern_ms,
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('gc_sample_kernel', kern_ms), kernel_ms=kern_ms,
                       alg_bytes_per_launch=per_sample * B),
-        extra=dict(fused_256x1024_samples_per_s=B * NB * reps * world / fdt, fused_256x1024_kernel_ms=fk_ms,
-                   fused_256x1024_achieved_GBs=per_sample * B * NB / (fk_ms * 1e-3) / 1e9),
+        extra=extra,
     )
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline_gc(data, cfg, B, args)
@@ -335,6 +360,7 @@ def bench_powder(args, world, rank, dev):
     # write H*W on one step in three, action 4, reward 4, flags 3, ctrl 16.
     per_step = size * size * 6 + size * size + size * size / 3 + 27
     achieved = per_step * n / (kern_ms * 1e-3) / 1e9
+    extra = {}
     K = 48
     fk_actions = actions[:K].contiguous()
     out = None
@@ -343,10 +369,13 @@ def bench_powder(args, world, rank, dev):
         nonlocal out
         out = env.rollout(fk_actions, out=out)
 
-    fused(0)
-    reps = max(1, steps // K)
-    fdt = _timed(fused, reps, world, dev)
-    fk_ms = _per_launch_ms(fused, 3, dev)
+    if not args.no_extras:
+        fused(0)
+        reps = max(1, steps // K)
+        fdt = _timed(fused, reps, world, dev)
+        fk_ms = _per_launch_ms(fused, 3, dev)
+        extra = dict(fused_k48_steps_per_s=n * K * reps * world / fdt, fused_k48_kernel_ms=fk_ms,
+                     fused_k48_achieved_GBs=per_step * n * K / (fk_ms * 1e-3) / 1e9)
     result = dict(
         metric='env steps/sec, powderworld-easy-v0 64x64, N=4096 parallel envs per GPU',
         value=value, unit='env_steps/s', n_gpus=world, steps=steps, warmup=args.warmup,
@@ -355,10 +384,9 @@ def bench_powder(args, world, rank, dev):
         config=dict(workload='powderworld-easy-v0 world_size=64', num_envs_per_gpu=n, auto_reset=True,
                     parallelism=f'env-shard x{world}'),
         roofline=dict(bound='hbm', kernel='pw_step_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=None, kernel_ms=kern_ms,
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('pw_step_kernel', kern_ms), kernel_ms=kern_ms,
                       alg_bytes_per_launch=per_step * n),
-        extra=dict(fused_k48_steps_per_s=n * K * reps * world / fdt, fused_k48_kernel_ms=fk_ms,
-                   fused_k48_achieved_GBs=per_step * n * K / (fk_ms * 1e-3) / 1e9),
+        extra=extra,
     )
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result['cpu_baseline'] = cpu_baseline_powder(size, args)
@@ -399,6 +427,7 @@ def main():
     ap.add_argument('--ring', type=int, default=128)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-extras', action='store_true', help='only the timed single-step workload (profiling runs)')
     args = ap.parse_args()
     world, rank, local = _dist_init()
     if world != args.gpus and rank == 0:

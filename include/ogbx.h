@@ -328,6 +328,22 @@ ogbx_status ogbx_powder_state(ogbx_powder_t env, uint8_t** world, int32_t** ctrl
 ogbx_status ogbx_powder_forward(ogbx_powder_t env, const uint8_t* world_in, int64_t n_worlds,
                                 int32_t steps, uint8_t* world_out, void* stream);
 
+/* ======================================================================
+ * Evaluation counters (impls/utils/evaluation.py:36-123, impls/main.py:226-258)
+ * ====================================================================== */
+
+/* For every env i whose episode ended at this step (terminated[i] |
+ * truncated[i]) while remaining[i] > 0: counters[task_id[i]-1] += {success[i],
+ * 1} and remaining[i] -= 1.  All pointers are device memory: success /
+ * terminated / truncated u8[n] (a step's outputs), task_id i32[n] (1-based),
+ * remaining i32[n] (in/out), counters int64[num_tasks, 2] = {success_sum,
+ * episode_count} (accumulated, never cleared here; num_tasks <= 64).  The
+ * counter block is what ranks all-gather at the end of evaluation. */
+ogbx_status ogbx_eval_accumulate(const uint8_t* success, const uint8_t* terminated,
+                                 const uint8_t* truncated, const int32_t* task_id,
+                                 int32_t* remaining, int64_t n, int32_t num_tasks, int64_t* counters,
+                                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

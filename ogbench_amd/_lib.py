@@ -94,6 +94,10 @@ _SIGNATURES = {
     ),
     'ogbx_powder_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p)]),
     'ogbx_powder_forward': (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    # evaluation
+    'ogbx_eval_accumulate': (
+        c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]
+    ),
 }
 
 _lock = threading.Lock()

@@ -1,13 +1,26 @@
 #!/bin/bash
-# rocprofv3 kernel-trace summary of a short bench run (no PMC counters here).
+# rocprofv3 evidence for one bench workload (run on the GPU box):
+#   1. --kernel-trace --stats   (per-kernel durations)
+#   2. --pmc FETCH_SIZE         (own pass: TCC slots cannot hold both)
+#   3. --pmc WRITE_SIZE
+# then (locally, after gpurun merged gpurun_out/) scripts/prof_summary.py -> profiles/<round>_<wl>_kernel_stats.csv and
+# profiles/traffic.json.  Usage: WL=powder KERNEL=pw_step_kernel ROUND=r01 scripts/gpu_prof.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+REPO=$(pwd)
+WL=${WL:-pointmaze}
+KERNEL=${KERNEL:-maze_step_kernel}
+ROUND=${ROUND:-r01}
+STEPS=${STEPS:-300}
 mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp
-cd "${GRAFT_REPO_ROOT:-$OLDPWD}"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- \
-  python3 bench.py --steps ${STEPS:-300} --warmup 20 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof_bench.log 2>&1
-rc=$?
-tail -2 gpurun_out/prof_bench.log
-find gpurun_out/prof -name "*stats*" | head
-exit $rc
+export TMPDIR=/tmp
+ARGS="--workload $WL --steps $STEPS --warmup 20 --no-cpu-baseline --no-extras"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$WL -o run --output-format csv -- \
+  python3 bench.py $ARGS > gpurun_out/prof_${WL}.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$WL -o run --output-format csv -- \
+  python3 bench.py $ARGS > gpurun_out/pmc_fetch_${WL}.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$WL -o run --output-format csv -- \
+  python3 bench.py $ARGS > gpurun_out/pmc_write_${WL}.log 2>&1 || exit $?
+tail -1 gpurun_out/prof_${WL}.log
+# profiles/ is written back here (gpurun returns only gpurun_out/):
+#   python3 scripts/prof_summary.py --round $ROUND --workload $WL --kernel $KERNEL
