@@ -72,11 +72,18 @@ def _timed(fn, steps, world, dev):
     return _max_over_ranks(dt, world, dev)
 
 
-def _per_launch_ms(fn, launches, dev):
+def _per_launch_ms(fn, launches, dev, host_us=120.0):
     """Average device duration of single launches: HIP event pair around each
-    launch, on the stream the kernel runs on (torch's current stream)."""
+    launch, on the stream the kernel runs on (torch's current stream).
+
+    A spin kernel (torch.cuda._sleep) is queued first, long enough for the host
+    to enqueue every event pair and launch behind it; the pairs then time the
+    kernels back to back instead of the host's launch gaps (a host-bound call
+    such as GCDataset.sample(1024) would otherwise read as its host time)."""
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    torch.cuda.synchronize(dev)
+    torch.cuda._sleep(int(launches * host_us * 1e-6 * 2.4e9))
     for i, (a, b) in enumerate(ev):
         a.record(stream)
         fn(i)
