@@ -481,6 +481,7 @@ static PointModel make_point_model(double unit, double off) {
   pm.inv_M2w = 1.0 / (M + 2.0 * w);
   pm.inv_M4w = 1.0 / (M + 4.0 * w);
   pm.inv_det3 = 1.0 / ((M + 3.0 * w) * (M + w) - w * w);
+  pm.inv_width = 1.0 / pm.imp_width;
   return pm;
 }
 

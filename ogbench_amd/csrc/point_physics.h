@@ -54,6 +54,7 @@ struct PointModel {
   double w_max;       // D of an edge at imp = dmax (|dist| >= width)
   double kp_max;      // K * dmax
   double inv_M2w, inv_M4w, inv_det3;  // closed-form reciprocals at w = w_max
+  double inv_width;   // 1 / solimp width
   int32_t nsub;       // frame_skip (5)
   int32_t pad_;
 };
@@ -118,32 +119,37 @@ __device__ __forceinline__ const ContactSlot& slot_of(const Contacts& c, int k) 
   return k == 0 ? c.s0 : (k == 1 ? c.s1 : c.s2);
 }
 
-// Store one contact into slot `slot`.  imp = MuJoCo getimpedance() with solimp
-// power 2; beyond the transition width it is dmax and D, K*imp are the
-// precomputed constants (the quotient dist/width is only formed near the
-// transition, where it decides the sigmoid).  Slot 0 (the common case) is a
-// direct write; slots 1..2 use static predicated writes (no scratch).
-__device__ __forceinline__ void add_contact(const PointModel& pm, Contacts& c, int slot, double dist,
-                                   double nx, double ny, double tx, double ty) {
-  double D = pm.w_max, kp = pm.kp_max * dist;
-  if (fabs(dist) < 2.0 * pm.imp_width) {
-    const double x = fabs(dist / pm.imp_width);
-    if (x < 1.0) {
-      double imp;
-      if (x <= 0.0) {
-        imp = pm.imp_dmin;
-      } else {
-        const double y = x <= pm.imp_mid ? pm.imp_a * (x * x) : 1.0 - pm.imp_b * ((1.0 - x) * (1.0 - x));
-        imp = pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
-      }
-      double R = (1.0 - imp) * pm.diag / imp;
-      if (R < kMinVal) R = kMinVal;
-      D = 1.0 / R;
-      kp = pm.K * imp * dist;
+// Impedance-dependent (D, K*imp*dist) of a contact at `dist` (MuJoCo
+// getimpedance, solimp power 2).  Beyond the transition width these are the
+// precomputed constants.  Inside it: x = |dist|/width (as a product with the
+// host-rounded reciprocal) and D = 1/R = imp / ((1-imp)*diag) (one division;
+// R >= (1-dmax)/dmax*diag never reaches mjMINVAL).  Both differ from MuJoCo's
+// literal quotients by at most an ulp (contact path tolerance 1e-9).
+__device__ __forceinline__ void contact_gains(const PointModel& pm, double dist, double* D,
+                                              double* kp) {
+  *D = pm.w_max;
+  *kp = pm.kp_max * dist;
+  const double x = fabs(dist) * pm.inv_width;
+  if (x < 1.0) {
+    double imp;
+    if (x <= 0.0) {
+      imp = pm.imp_dmin;
+    } else {
+      const double y = x <= pm.imp_mid ? pm.imp_a * (x * x) : 1.0 - pm.imp_b * ((1.0 - x) * (1.0 - x));
+      imp = pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
     }
+    *D = imp / ((1.0 - imp) * pm.diag);
+    *kp = pm.K * imp * dist;
   }
-  // Per-field selects (not branches): a branchy store would be merged by
-  // SimplifyCFG into one store through a selected address -> scratch.
+}
+
+// Store one contact into slot `slot` (runtime index, per-field selects: a
+// branchy store would be merged by SimplifyCFG into one store through a
+// selected address -> scratch).
+__device__ __forceinline__ void add_contact(const PointModel& pm, Contacts& c, int slot, double dist,
+                                            double nx, double ny, double tx, double ty) {
+  double D, kp;
+  contact_gains(pm, dist, &D, &kp);
   auto put = [&](ContactSlot& d, bool on) {
     d.nx = on ? nx : d.nx;
     d.ny = on ? ny : d.ny;
@@ -157,118 +163,96 @@ __device__ __forceinline__ void add_contact(const PointModel& pm, Contacts& c, i
   put(c.s2, slot == 2);
 }
 
-// Exact sphere-box test of the wall box centred at (cx, cy) (MuJoCo sphere-box
-// collision in the box frame; boxes are axis aligned, margin 0).  Appends to
-// `c` on contact.
-__device__ __forceinline__ void collide_box(const PointModel& pm, double x, double y, double cx, double cy,
-                                   Contacts& c, int& nc) {
-  const double hx = pm.box_hxy, hz = pm.box_hz;
-  const double px = x - cx;
-  const double py = y - cy;
-  const double pz = pm.sphere_z - pm.box_cz;
-  const double clx = px < -hx ? -hx : (px > hx ? hx : px);
-  const double cly = py < -hx ? -hx : (py > hx ? hx : py);
-  const double clz = pz < -hz ? -hz : (pz > hz ? hz : pz);
-  const double tx = clx - px, ty = cly - py, tz = clz - pz;
-  const double d2 = tx * tx + ty * ty + tz * tz;
-  if (d2 > pm.r2_hi || nc >= kMaxContacts) return;  // certainly d - r > 0
-  // Face contacts (one of tx, ty zero; tz is 0 for every wall) need neither
-  // sqrt nor division: sqrt(fl(t*t)) == |t| and -t/|t| == -sign(t) exactly.
-  double d, nx, ny;
-  if (ty == 0.0 && tz == 0.0) {
-    d = fabs(tx);
-    nx = tx > 0.0 ? -1.0 : 1.0;
-    ny = -0.0 * ty;
-  } else if (tx == 0.0 && tz == 0.0) {
-    d = fabs(ty);
-    nx = -0.0 * tx;
-    ny = ty > 0.0 ? -1.0 : 1.0;
-  } else {
-    d = sqrt(d2);
-    const double inv = 1.0 / d;
-    nx = -tx * inv;
-    ny = -ty * inv;
-  }
-  if (d - pm.radius > 0.0) return;
-  if (d > kMinVal) {
-    // centre outside the box: normal along (centre - closest point).
-    add_contact(pm, c, nc, d - pm.radius, nx, ny, -ny, nx);
-  } else {
-    // centre inside the box: push out through the nearest face
-    // (faces ordered -x, +x, -y, +y, -z, +z; first strict minimum wins).
-    const double f0 = hx + px, f1 = hx - px, f2 = hx + py, f3 = hx - py, f4 = hz + pz,
-                 f5 = hz - pz;
-    int k = 0;
-    double best = f0;
-    if (f1 < best) { best = f1; k = 1; }
-    if (f2 < best) { best = f2; k = 2; }
-    if (f3 < best) { best = f3; k = 3; }
-    if (f4 < best) { best = f4; k = 4; }
-    if (f5 < best) { best = f5; k = 5; }
-    const double dist = -best - pm.radius;
-    const double sgn = (k & 1) ? 1.0 : -1.0;
-    if (k < 2) {
-      add_contact(pm, c, nc, dist, sgn, 0.0, 0.0, 1.0);
-    } else if (k < 4) {
-      add_contact(pm, c, nc, dist, 0.0, sgn, 1.0, 0.0);
-    } else {
-      // z face: Jn = 0, tangents e_x and e_y -> two pseudo-contacts.
-      add_contact(pm, c, nc, dist, 0.0, 0.0, 1.0, 0.0);
-      if (nc + 1 < kMaxContacts) add_contact(pm, c, ++nc, dist, 0.0, 0.0, 0.0, 1.0);
-    }
-  }
-  ++nc;
-}
-
-// Impedance-dependent (D, K*imp*dist) of a contact at `dist` (MuJoCo
-// getimpedance, solimp power 2).  Outside the transition width these are the
-// precomputed constants; `dist / width` is formed only near the transition.
-__device__ __forceinline__ void contact_gains(const PointModel& pm, double dist, double* D,
-                                              double* kp) {
-  *D = pm.w_max;
-  *kp = pm.kp_max * dist;
-  if (fabs(dist) < 2.0 * pm.imp_width) {
-    const double x = fabs(dist / pm.imp_width);
-    if (x < 1.0) {
-      double imp;
-      if (x <= 0.0) {
-        imp = pm.imp_dmin;
-      } else {
-        const double y = x <= pm.imp_mid ? pm.imp_a * (x * x) : 1.0 - pm.imp_b * ((1.0 - x) * (1.0 - x));
-        imp = pm.imp_dmin + y * (pm.imp_dmax - pm.imp_dmin);
-      }
-      double R = (1.0 - imp) * pm.diag / imp;
-      if (R < kMinVal) R = kMinVal;
-      *D = 1.0 / R;
-      *kp = pm.K * imp * dist;
-    }
-  }
-}
-
 __device__ __forceinline__ void zero_slot(ContactSlot& k) {
   k.nx = 0.0; k.ny = 0.0; k.tx = 0.0; k.ty = 0.0; k.kp = 0.0; k.w = 0.0;
 }
 
 // Generic (slow, rare) collision: the sphere centre is in a wall cell, off the
-// map, or exactly on a box face.  Same exact per-box test as the fast path.
+// map, or exactly on a box face.  Exact sphere-box test (MuJoCo sphere-box in
+// the box frame; boxes axis aligned, margin 0) of the own cell's box and the
+// x-side, y-side and diagonal neighbours, in that order.  One rolled loop with
+// one contact-append site keeps this path small (it is inlined).
 __device__ __forceinline__ int collide_walls_generic(const PointModel& pm, const uint16_t* nbmask,
-                                                  int H, int W, double x, double y, double fi,
-                                                  double fj, int sx, int sy, Contacts& c) {
+                                                     int H, int W, double x, double y, double fi,
+                                                     double fj, int sx, int sy, Contacts& c) {
   zero_slot(c.s0);
   zero_slot(c.s1);
   zero_slot(c.s2);
   const double cx = fj * pm.unit - pm.off_x, cy = fi * pm.unit - pm.off_y;
-  const double u = pm.unit;
-  auto wall_at = [&](int di, int dj) -> bool {
-    const double ii = fi + di, jj = fj + dj;
-    if (!(ii >= 0.0 && ii < (double)H && jj >= 0.0 && jj < (double)W)) return false;
-    return (nbmask[(int)ii * W + (int)jj] >> 4) & 1u;  // the cell's own wall bit
-  };
+  const double u = pm.unit, hx = pm.box_hxy, hz = pm.box_hz;
   int nc = 0;
-  if (wall_at(0, 0)) collide_box(pm, x, y, cx, cy, c, nc);
-  if (sx != 0 && wall_at(0, sx)) collide_box(pm, x, y, cx + sx * u, cy, c, nc);
-  if (sy != 0 && wall_at(sy, 0)) collide_box(pm, x, y, cx, cy + sy * u, c, nc);
-  if (sx != 0 && sy != 0 && wall_at(sy, sx)) collide_box(pm, x, y, cx + sx * u, cy + sy * u, c, nc);
+#pragma unroll 1
+  for (int b = 0; b < 4; ++b) {
+    const int dj = (b & 1) ? sx : 0;  // b: 0 own cell, 1 x side, 2 y side, 3 diagonal
+    const int di = (b & 2) ? sy : 0;
+    if ((b == 1 && sx == 0) || (b == 2 && sy == 0) || (b == 3 && (sx == 0 || sy == 0))) continue;
+    const double ii = fi + di, jj = fj + dj;
+    if (!(ii >= 0.0 && ii < (double)H && jj >= 0.0 && jj < (double)W)) continue;
+    if (!((nbmask[(int)ii * W + (int)jj] >> 4) & 1u)) continue;  // the cell's own wall bit
+    const double px = x - (cx + dj * u);
+    const double py = y - (cy + di * u);
+    const double pz = pm.sphere_z - pm.box_cz;
+    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
+    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    const double clz = pz < -hz ? -hz : (pz > hz ? hz : pz);
+    const double tx = clx - px, ty = cly - py, tz = clz - pz;
+    const double d2 = tx * tx + ty * ty + tz * tz;
+    if (d2 > pm.r2_hi || nc >= kMaxContacts) continue;  // certainly d - r > 0
+    double dist, nx, ny, ax, ay;  // ax, ay: tangent of the (first) contact
+    int ne = 1;
+    bool second = false;          // z face: two pseudo-contacts (tangents e_x, e_y)
+    // Face contacts need neither sqrt nor division: sqrt(fl(t*t)) == |t|.
+    double d;
+    if (ty == 0.0 && tz == 0.0) {
+      d = fabs(tx);
+      nx = tx > 0.0 ? -1.0 : 1.0;
+      ny = -0.0 * ty;
+    } else if (tx == 0.0 && tz == 0.0) {
+      d = fabs(ty);
+      nx = -0.0 * tx;
+      ny = ty > 0.0 ? -1.0 : 1.0;
+    } else {
+      d = sqrt(d2);
+      nx = -tx / d;
+      ny = -ty / d;
+    }
+    if (d - pm.radius > 0.0) continue;
+    if (d > kMinVal) {
+      // centre outside the box: normal along (centre - closest point).
+      dist = d - pm.radius;
+      ax = -ny;
+      ay = nx;
+    } else {
+      // centre inside the box: push out through the nearest face
+      // (faces ordered -x, +x, -y, +y, -z, +z; first strict minimum wins).
+      const double f0 = hx + px, f1 = hx - px, f2 = hx + py, f3 = hx - py, f4 = hz + pz,
+                   f5 = hz - pz;
+      int k = 0;
+      double best = f0;
+      if (f1 < best) { best = f1; k = 1; }
+      if (f2 < best) { best = f2; k = 2; }
+      if (f3 < best) { best = f3; k = 3; }
+      if (f4 < best) { best = f4; k = 4; }
+      if (f5 < best) { best = f5; k = 5; }
+      dist = -best - pm.radius;
+      const double sgn = (k & 1) ? 1.0 : -1.0;
+      if (k < 2) {
+        nx = sgn; ny = 0.0; ax = 0.0; ay = 1.0;
+      } else if (k < 4) {
+        nx = 0.0; ny = sgn; ax = 1.0; ay = 0.0;
+      } else {
+        nx = 0.0; ny = 0.0; ax = 1.0; ay = 0.0;
+        second = true;
+        ne = 2;
+      }
+    }
+#pragma unroll 1
+    for (int e = 0; e < ne && nc < kMaxContacts; ++e) {
+      const bool z2 = second && e == 1;
+      add_contact(pm, c, nc, dist, nx, ny, z2 ? 0.0 : ax, z2 ? 1.0 : ay);
+      ++nc;
+    }
+  }
   c.n = nc;
   return nc;
 }
@@ -335,19 +319,20 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
   bool cD = vD && d2D <= pm.r2_hi;
   // exact-geometry guards: face roles must really be faces, d > mjMINVAL
   slow = slow || (cX && (tXy != 0.0 || dX <= kMinVal)) || (cY && (tYx != 0.0 || dY <= kMinVal));
-  if (__builtin_expect(slow, 0)) return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
   double dD = 0.0, nDx = 0.0, nDy = 0.0;
-  if (cD) {  // vertical-edge contact of the diagonal box
+  if (cD && !slow) {  // vertical-edge contact of the diagonal box
     dD = sqrt(d2D);
     if (dD - r > 0.0) {
       cD = false;
     } else if (dD <= kMinVal) {
-      return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
+      slow = true;
     } else {
-      nDx = -tDx / dD;
-      nDy = -tDy / dD;
+      const double inv = 1.0 / dD;
+      nDx = -tDx * inv;
+      nDy = -tDy * inv;
     }
   }
+  if (__builtin_expect(slow, 0)) return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
   double D, kp;
   // s0: x face, n = (-sign(tx), -ty) with ty = +-0
   contact_gains(pm, dX - r, &D, &kp);
@@ -390,6 +375,7 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
 // Returns false if rounding leaves none consistent (caller falls back).
 __device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Contacts& c, double cux,
                                          double cuy, double* ux, double* uy) {
+#pragma clang fp contract(fast)
   const double M = pm.M;
   // exactly one slot is non-zero (the others are all-zero): sum them
   const double nx = c.s0.nx + c.s1.nx + c.s2.nx, ny = c.s0.ny + c.s1.ny + c.s2.ny;
@@ -423,38 +409,49 @@ __device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Co
     const double dmn = (a22 * r1 + w * rm2) * idet, dmt = (a11 * rm2 + w * r1) * idet;
     // {0,+,-}: decoupled
     const double fn = (M * cn - 4.0 * w * e) * i4, ft = M * ct * i2;
-    if (bpn + e + bpt < 0.0 && bpn + e - bpt >= 0.0 && bpn + e >= 0.0) {
-      un = bpn; ut = bpt;
-    } else if (bmn + e - bmt < 0.0 && bmn + e + bmt >= 0.0 && bmn + e >= 0.0) {
-      un = bmn; ut = bmt;
-    } else if (dpn + e < 0.0 && dpn + e + dpt < 0.0 && dpn + e - dpt >= 0.0) {
-      un = dpn; ut = dpt;
-    } else if (dmn + e < 0.0 && dmn + e - dmt < 0.0 && dmn + e + dmt >= 0.0) {
-      un = dmn; ut = dmt;
-    } else if (fn + e + ft < 0.0 && fn + e - ft < 0.0) {
-      un = fn; ut = ft;
-    } else {
-      ok = false;
-    }
+    // consistency of each candidate set; the first consistent one wins
+    // (selects, not a branch chain: every candidate is already computed)
+    const bool kP = bpn + e + bpt < 0.0 && bpn + e - bpt >= 0.0 && bpn + e >= 0.0;
+    const bool kM = bmn + e - bmt < 0.0 && bmn + e + bmt >= 0.0 && bmn + e >= 0.0;
+    const bool kDP = dpn + e < 0.0 && dpn + e + dpt < 0.0 && dpn + e - dpt >= 0.0;
+    const bool kDM = dmn + e < 0.0 && dmn + e - dmt < 0.0 && dmn + e + dmt >= 0.0;
+    const bool kF = fn + e + ft < 0.0 && fn + e - ft < 0.0;
+    un = kF ? fn : un;
+    ut = kF ? ft : ut;
+    un = kDM ? dmn : un;
+    ut = kDM ? dmt : ut;
+    un = kDP ? dpn : un;
+    ut = kDP ? dpt : ut;
+    un = kM ? bmn : un;
+    ut = kM ? bmt : ut;
+    un = kP ? bpn : un;
+    ut = kP ? bpt : ut;
+    ok = kP || kM || kDP || kDM || kF;
   }
   *ux = un * nx + ut * tx;
   *uy = un * ny + ut * ty;
   return ok;
 }
 
-// Residuals, gradient and Hessian of f at u.  Returns the active-edge mask.
-__device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Contacts& c, double cux,
-                                      double cuy, double ux, double uy, double* g, double* h,
-                                      double* fval) {
+// Residuals, gradient and Hessian (and optionally f) at u.  Returns the
+// active-edge mask.  `live` has bit s set when some lane of the wave holds a
+// contact in slot s (wave-uniform): empty slots are all-zero rows (r = 0,
+// never active), so skipping a slot no lane uses changes nothing.
+template <bool kWithF>
+__device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Contacts& c, uint32_t live,
+                                               double cux, double cuy, double ux, double uy, double* g,
+                                               double* h, double* fval) {
+#pragma clang fp contract(fast)
   const double M = pm.M;
   g[0] = M * (ux - cux);
   g[1] = M * (uy - cuy);
   h[0] = M; h[1] = 0.0; h[2] = M;
-  double f = 0.5 * M * ((ux - cux) * (ux - cux) + (uy - cuy) * (uy - cuy));
+  double f = 0.0;
+  if (kWithF) f = 0.5 * M * ((ux - cux) * (ux - cux) + (uy - cuy) * (uy - cuy));
   uint32_t act = 0;
 #pragma unroll
   for (int s = 0; s < kMaxContacts; ++s) {
-    {  // empty slots are all-zero: r = 0 is never < 0, so their rows are inactive
+    if (live & (1u << s)) {
       const ContactSlot& k = slot_of(c, s);
       const double a = k.nx * ux + k.ny * uy + k.kp;
       const double b = k.tx * ux + k.ty * uy;
@@ -462,48 +459,74 @@ __device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Conta
       for (int e = 0; e < 3; ++e) {
         const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
         const double r = e == 2 ? a : a + sg * b;
-        if (r < 0.0) {
-          const double we = e == 2 ? 2.0 * k.w : k.w;
-          const double jx = e == 2 ? k.nx : k.nx + sg * k.tx;
-          const double jy = e == 2 ? k.ny : k.ny + sg * k.ty;
-          act |= 1u << (3 * s + e);
-          g[0] += we * r * jx;
-          g[1] += we * r * jy;
-          h[0] += we * jx * jx;
-          h[1] += we * jx * jy;
-          h[2] += we * jy * jy;
-          f += 0.5 * we * r * r;
-        }
+        // branch-free: an inactive row contributes with weight 0
+        const bool on = r < 0.0;
+        const double we = on ? (e == 2 ? 2.0 * k.w : k.w) : 0.0;
+        const double jx = e == 2 ? k.nx : k.nx + sg * k.tx;
+        const double jy = e == 2 ? k.ny : k.ny + sg * k.ty;
+        act |= (on ? 1u : 0u) << (3 * s + e);
+        const double wr = we * r, wjx = we * jx;
+        g[0] += wr * jx;
+        g[1] += wr * jy;
+        h[0] += wjx * jx;
+        h[1] += wjx * jy;
+        h[2] += (we * jy) * jy;
+        if (kWithF) f += 0.5 * wr * r;
       }
     }
   }
-  *fval = f;
+  if (kWithF) *fval = f;
+  return act;
+}
+
+// Active-edge mask at u only (no derivatives).
+__device__ __forceinline__ uint32_t active_set(const Contacts& c, uint32_t live, double ux, double uy) {
+#pragma clang fp contract(fast)
+  uint32_t act = 0;
+#pragma unroll
+  for (int s = 0; s < kMaxContacts; ++s) {
+    if (live & (1u << s)) {
+      const ContactSlot& k = slot_of(c, s);
+      const double a = k.nx * ux + k.ny * uy + k.kp;
+      const double b = k.tx * ux + k.ty * uy;
+      act |= (a + b < 0.0 ? 1u : 0u) << (3 * s);
+      act |= (a - b < 0.0 ? 1u : 0u) << (3 * s + 1);
+      act |= (a < 0.0 ? 1u : 0u) << (3 * s + 2);
+    }
+  }
   return act;
 }
 
 // Several contacts: full-step semismooth Newton from the warm start *u_io
 // (the previous RK stage's solution; the optimum is unique, so the start only
-// changes the iteration count).  u is optimal once the active set at the
-// Newton point equals the set the step was computed on.  Safety net: damped
-// Newton with Armijo backtracking from cu (monotone, globally convergent).
-__device__ __forceinline__ void solve_newton(const PointModel& pm, const Contacts& c, double cux,
-                                    double cuy, double* ux_io, double* uy_io) {
+// changes the iteration count).  A full Newton step on the quadratic piece of
+// active set A lands on that piece's minimiser; if the active set there is
+// still A, the gradient of f vanishes and the point is the optimum (one
+// derivative evaluation + one mask evaluation per converged stage).  Safety
+// net: damped Newton with Armijo backtracking from cu (monotone, globally
+// convergent).
+__device__ __forceinline__ void solve_newton(const PointModel& pm, const Contacts& c, uint32_t live,
+                                             double cux, double cuy, double* ux_io, double* uy_io) {
+#pragma clang fp contract(fast)
   double ux = *ux_io, uy = *uy_io;
   double g[2], h[3], f;
-  uint32_t prev = 0xFFFFFFFFu;
   bool done = false;
+  uint32_t act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
 #pragma unroll 1
   for (int it = 0; it < 8; ++it) {
-    const uint32_t act = eval_piece(pm, c, cux, cuy, ux, uy, g, h, &f);
     OGBX_STAT(4);
-    if (act == prev || (g[0] == 0.0 && g[1] == 0.0)) {
+    if (g[0] == 0.0 && g[1] == 0.0) {
       done = true;
       break;
     }
     const double idet = 1.0 / (h[0] * h[2] - h[1] * h[1]);
     ux -= (h[2] * g[0] - h[1] * g[1]) * idet;
     uy -= (h[0] * g[1] - h[1] * g[0]) * idet;
-    prev = act;
+    if (active_set(c, live, ux, uy) == act) {
+      done = true;
+      break;
+    }
+    act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
   }
   if (!done) {
     OGBX_STAT(5);
@@ -511,7 +534,7 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
     uy = cuy;
 #pragma unroll 1
     for (int it = 0; it < 64; ++it) {
-      eval_piece(pm, c, cux, cuy, ux, uy, g, h, &f);
+      eval_piece<true>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
       const double idet = 1.0 / (h[0] * h[2] - h[1] * h[1]);
       const double px = -(h[2] * g[0] - h[1] * g[1]) * idet;
       const double py = -(h[0] * g[1] - h[1] * g[0]) * idet;
@@ -520,7 +543,7 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
       double t = 1.0, g2[2], h2[3], f2;
 #pragma unroll 1
       for (int bt = 0; bt < 60; ++bt) {
-        eval_piece(pm, c, cux, cuy, ux + t * px, uy + t * py, g2, h2, &f2);
+        eval_piece<true>(pm, c, live, cux, cuy, ux + t * px, uy + t * py, g2, h2, &f2);
         if (f2 <= f + 1e-6 * t * slope) break;
         t *= 0.5;
       }
@@ -541,6 +564,7 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
 __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& c, double vx,
                                           double vy, double* ax_out, double* ay_out, double* wx,
                                           double* wy) {
+#pragma clang fp contract(fast)
   const double bvx = pm.B * vx, bvy = pm.B * vy;
   const double cux = pm.m_over_M * bvx, cuy = pm.m_over_M * bvy;  // floor-only minimiser
   double ux = cux, uy = cuy;
@@ -557,7 +581,11 @@ __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& 
     need_newton = false;
 #endif
   }
-  if (need_newton) solve_newton(pm, c, cux, cuy, &ux, &uy);
+  if (need_newton) {
+    const uint32_t live = (__any(c.s0.w != 0.0) ? 1u : 0u) | (__any(c.s1.w != 0.0) ? 2u : 0u) |
+                          (__any(c.s2.w != 0.0) ? 4u : 0u);
+    solve_newton(pm, c, live, cux, cuy, &ux, &uy);
+  }
   *wx = ux;
   *wy = uy;
   *ax_out = ux - bvx;
@@ -601,6 +629,8 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
     OGBX_STAMP_SEG(_ta);
     solve_acc(pm, c, vsx, vsy, &fx, &fy, &wux, &wuy);
     OGBX_STAMP_SEG(_tb);
+    {
+#pragma clang fp contract(fast)
     const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
     sqx = sqx + b * vsx;
     sqy = sqy + b * vsy;
@@ -623,6 +653,7 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
       vsx = vx;
       vsy = vy;
       sqx = sqy = svx = svy = 0.0;
+    }
     }
     OGBX_STAMP_SEG(_tc);
   }
