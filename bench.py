@@ -29,18 +29,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def _dist_init():
+def _dist_init(backend='nccl'):
+    """One process per GPU.  backend 'nccl' is RCCL; 'gloo' (with ranks sharing
+    GPUs: device = LOCAL_RANK mod device count) rehearses the N>1 path on a
+    one-GPU box."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    ndev = max(1, torch.cuda.device_count())
+    dev_index = local % ndev if backend == 'gloo' else local
+    torch.cuda.set_device(dev_index)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(local)
-    return world, rank, local
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev_index))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, dev_index
 
 
 def _barrier(world):
@@ -55,7 +61,8 @@ def _max_over_ranks(x, world, dev):
         return x
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    on_dev = dist.get_backend() == 'nccl'
+    t = torch.tensor([x], dtype=torch.float64, device=dev if on_dev else 'cpu')
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -136,7 +143,7 @@ def bench_pointmaze(args, world, rank, dev):
     alg_bytes = 87 * n  # 87 B per env-step
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
-    extra = {}
+    extra = {'eval_allgather': _eval_allgather(env, actions, world, dev)}
     if args.no_extras:
         return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
     # hipGraph replay of G steps (launch-bound inner loop captured once)
@@ -177,6 +184,30 @@ def bench_pointmaze(args, world, rank, dev):
     extra['fused_k64_kernel_ms'] = fk_ms
     extra['fused_k64_achieved_GBs'] = fused_bytes / (fk_ms * 1e-3) / 1e9
     return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
+
+
+def _eval_allgather(env, actions, world, dev, steps=200):
+    """Untimed: the eval success reduction of SURVEY section 8e -- per-task
+    {success, episodes} counters accumulated on the device for `steps` steps,
+    then all-gathered over the process group (RCCL over xGMI at N>1)."""
+    from ogbench_amd.evaluation import accumulate, env_task_ids, gather_counters, summarize
+
+    counters = torch.zeros(env.num_tasks, 2, dtype=torch.int64, device=dev)
+    remaining = torch.full((env.num_envs,), 1 << 30, dtype=torch.int32, device=dev)
+    tid = env_task_ids(env)
+    for i in range(steps):
+        _, _, term, trunc, info = env.step(actions[i % actions.shape[0]])
+        accumulate(counters, info['success'].view(torch.uint8), term.view(torch.uint8), trunc.view(torch.uint8),
+                   tid, remaining)
+    _barrier(world)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    total, per_rank = gather_counters(counters)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3
+    m = summarize(total, env.task_infos)
+    return dict(episodes=int(total[:, 1].sum()), ranks=int(per_rank.shape[0]),
+                overall_success=m.get('evaluation/overall_success'), allgather_ms=ms)
 
 
 def _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env):
@@ -435,8 +466,10 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-extras', action='store_true', help='only the timed single-step workload (profiling runs)')
+    ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
+                    help="'gloo' rehearses the multi-rank path with ranks sharing GPUs")
     args = ap.parse_args()
-    world, rank, local = _dist_init()
+    world, rank, local = _dist_init(args.dist_backend)
     if world != args.gpus and rank == 0:
         print(f'# note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE', flush=True)
     dev = torch.device('cuda', local)

@@ -61,10 +61,10 @@ def gather_counters(counters, group=None):
         return counters.clone(), counters.unsqueeze(0).clone()
     world = dist.get_world_size(group)
     out = torch.empty((world,) + tuple(counters.shape), dtype=counters.dtype, device=counters.device)
-    if dist.get_backend(group) == 'gloo':
-        parts = list(out.unbind(0))
-        dist.all_gather(parts, counters.contiguous(), group=group)
-        out = torch.stack(parts)
+    if dist.get_backend(group) == 'gloo':  # host tensors (gloo's CUDA coverage is partial)
+        parts = [torch.empty(tuple(counters.shape), dtype=counters.dtype) for _ in range(world)]
+        dist.all_gather(parts, counters.detach().cpu().contiguous(), group=group)
+        out = torch.stack(parts).to(counters.device)
     else:
         dist.all_gather_into_tensor(out, counters.contiguous(), group=group)
     return out.sum(0), out
