@@ -257,6 +257,74 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
                            int64_t* actor_goal_out, double* masks, double* rewards,
                            const ogbx_gc_draw_record* record, void* stream);
 
+/* ---- HGCDataset (impls/utils/datasets.py:467-643) ------------------------
+ * Static config of the hierarchical sampler.  Subgoal steps are the resolved
+ * values of the reference's config (value/actor default to
+ * high_subgoal_steps, itself defaulting to subgoal_steps).  The four tables
+ * are device f64 arrays indexed by the clipped subgoal step count s in
+ * [0, K] (K = value_subgoal_steps for hv_*, low_subgoal_steps for lv_*):
+ * masks = 1 - (s < K), rewards = gc_negative ? -(1 - d^s)/(1 - d) : d^s (s < K),
+ * precomputed on the host with the reference's own float64 power. */
+typedef struct {
+  int64_t value_subgoal_steps;
+  int64_t low_subgoal_steps;
+  int64_t actor_subgoal_steps;
+  int32_t has_low_value_goals; /* config low_discount is not None */
+  int32_t pad;
+  double low_discount;
+  const double* hv_mask_table;
+  const double* hv_reward_table;
+  const double* lv_mask_table;
+  const double* lv_reward_table;
+} ogbx_hgc_config;
+
+/* Injected draws: the GC draws (pick, v_*, a_*) plus the low-level value goal
+ * draws (l_*: randint pick, geometric, two rand) in the reference call order. */
+typedef struct {
+  ogbx_gc_draws gc;
+  const int64_t* l_pick;
+  const int64_t* l_geom;
+  const double* l_u_traj;
+  const double* l_u_cur;
+} ogbx_hgc_draws;
+
+typedef struct {
+  ogbx_gc_draw_record gc;
+  int64_t* l_pick;
+  int64_t* l_geom;
+  double* l_u_traj;
+  double* l_u_cur;
+} ogbx_hgc_draw_record;
+
+/* Per-sample scalar outputs (device, [batch*num_batches]); index outputs
+ * may be NULL. */
+typedef struct {
+  int64_t* idxs;
+  int64_t* high_value_goal_idxs;
+  int64_t* high_actor_goal_idxs;
+  int64_t* low_value_goal_idxs;
+  int64_t* high_value_offsets;      /* int64, goal - idx */
+  int64_t* high_value_subgoal_steps;
+  double* high_value_masks;
+  double* high_value_rewards;
+  int64_t* low_value_subgoal_steps;
+  double* low_value_masks;
+  double* low_value_rewards;
+  double* masks;                    /* one-step: 1 - (idx == high value goal) */
+  double* rewards;
+} ogbx_hgc_outputs;
+
+/* HGCDataset.sample in ONE launch.  Column `select` codes: 0 idx, 1 next
+ * (min(idx+1, R-1)), 2 high value goal, 3 high actor goal, 4 high value next,
+ * 5 low value next, 6 low value goal, 7 high actor next, 8 low actor goal
+ * (min(idx + actor_subgoal_steps, final)), 9 low actor next. */
+ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                            const ogbx_hgc_config* hcfg, const ogbx_gc_column* cols,
+                            int32_t num_cols, int64_t batch, int64_t num_batches,
+                            const ogbx_hgc_draws* draws, uint64_t seed, uint64_t call_index,
+                            const ogbx_hgc_outputs* out, const ogbx_hgc_draw_record* record,
+                            void* stream);
+
 /* traj_end[r] = terminal_locs[searchsorted(terminal_locs, r, 'left')] for
  * r in [0, R): binary search per row over the sorted terminal_locs
  * (device int64 [num_terminals]).  datasets.py:186,309. */

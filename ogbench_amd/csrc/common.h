@@ -90,6 +90,7 @@ enum StreamTag : uint32_t {
   kTagPowderReset = 0x50570001u,
   kTagPowderAction = 0x50570002u,
   kTagGcSample = 0x47430001u,
+  kTagHgcSample = 0x47430002u,
 };
 
 inline void seed_key(uint64_t seed, uint32_t tag, uint32_t* k0, uint32_t* k1) {

@@ -170,6 +170,150 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
   }
 }
 
+// HGCDataset.compute_high_next_idxs (datasets.py:478-491) for one sample.
+__device__ inline void high_next(int64_t idx, int64_t fin, int64_t goal, int64_t K, int64_t* next,
+                                 int64_t* steps) {
+  int64_t st = K < fin - idx ? K : fin - idx;
+  const int64_t diff = goal - idx;
+  if (0 <= diff && diff < st) st = diff;
+  *steps = st;
+  *next = idx + st;
+}
+
+constexpr int kHgcSel = 10;
+
+// HGCDataset.sample (datasets.py:496-643): same tile structure as
+// gc_sample_kernel with ten row selectors and the hierarchical scalars.
+__global__ void __launch_bounds__(256) hgc_sample_kernel(
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, GcColumns cols, int32_t num_cols,
+    int64_t total, int tile, ogbx_hgc_draws dr, uint32_t k0, uint32_t k1, uint32_t call_lo,
+    uint32_t call_hi, double v_log_q, double a_log_q, double l_log_q, ogbx_hgc_outputs o,
+    ogbx_hgc_draw_record rec) {
+  __shared__ int64_t sel[kHgcSel][kGcMaxTile];
+  const int64_t base = (int64_t)blockIdx.x * tile;
+  const int n_here = (int)((total - base) < tile ? (total - base) : tile);
+  if (threadIdx.x < n_here) {
+    const int64_t s = base + threadIdx.x;
+    const uint64_t su = (uint64_t)s;
+    const uint32_t c0 = (uint32_t)su, c3 = (uint32_t)(su >> 32) ^ call_hi;
+    const u32x4 w0 = philox4x32_10({c0, call_lo, 0u, c3}, k0, k1);
+    const u32x4 w1 = philox4x32_10({c0, call_lo, 1u, c3}, k0, k1);
+    const u32x4 w2 = philox4x32_10({c0, call_lo, 2u, c3}, k0, k1);
+    const u32x4 w3 = philox4x32_10({c0, call_lo, 3u, c3}, k0, k1);
+    const u32x4 w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
+    const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
+    const ogbx_gc_draws& g = dr.gc;
+    int64_t idx, pick = -1;
+    if (g.idxs) {
+      idx = g.idxs[s];
+    } else {
+      pick = g.pick ? g.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
+      idx = buf.valid_idxs ? buf.valid_idxs[pick] : pick;
+    }
+    const int64_t fin = buf.traj_end[idx];
+    const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
+    GoalDraws v, a, l;
+    v.pick = g.v_pick ? g.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
+    a.pick = g.a_pick ? g.a_pick[s] : (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+    const double uvg = u01_from(w1.z, w1.w), uag = u01_from(w2.x, w2.y);
+    v.geom = g.v_geom ? g.v_geom[s] : (cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0);
+    a.geom = g.a_geom ? g.a_geom[s] : (cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0);
+    v.dist = g.v_dist ? g.v_dist[s] : uvg;
+    a.dist = g.a_dist ? g.a_dist[s] : uag;
+    v.u_traj = g.v_u_traj ? g.v_u_traj[s] : u01_from(w2.z, w2.w);
+    v.u_cur = g.v_u_cur ? g.v_u_cur[s] : u01_from(w3.x, w3.y);
+    a.u_traj = g.a_u_traj ? g.a_u_traj[s] : u01_from(w3.z, w3.w);
+    a.u_cur = g.a_u_cur ? g.a_u_cur[s] : u01_from(w4.x, w4.y);
+    const int64_t hvg = sample_goal(idx, fin, v, buf.valid_idxs, buf.num_valid, cfg.value_p_curgoal,
+                                    cfg.value_traj_thresh, cfg.value_geom_sample, cfg.value_cur_is_one);
+    const int64_t hag = sample_goal(idx, fin, a, buf.valid_idxs, buf.num_valid, cfg.actor_p_curgoal,
+                                    cfg.actor_traj_thresh, cfg.actor_geom_sample, cfg.actor_cur_is_one);
+    int64_t lvg = idx;
+    if (hc.has_low_value_goals) {
+      const u32x4 w5 = philox4x32_10({c0, call_lo, 5u, c3}, k0, k1);
+      const u32x4 w6 = philox4x32_10({c0, call_lo, 6u, c3}, k0, k1);
+      l.pick = dr.l_pick ? dr.l_pick[s] : (int64_t)bounded64(w5.x, w5.y, (uint64_t)npick);
+      l.geom = dr.l_geom ? dr.l_geom[s] : geometric_from(u01_from(w5.z, w5.w), l_log_q);
+      l.dist = 0.0;
+      l.u_traj = dr.l_u_traj ? dr.l_u_traj[s] : u01_from(w6.x, w6.y);
+      l.u_cur = dr.l_u_cur ? dr.l_u_cur[s] : u01_from(w6.z, w6.w);
+      lvg = sample_goal(idx, fin, l, buf.valid_idxs, buf.num_valid, cfg.value_p_curgoal,
+                        cfg.value_traj_thresh, 1, cfg.value_cur_is_one);
+      if (rec.l_pick) {
+        rec.l_pick[s] = l.pick;
+        rec.l_geom[s] = l.geom;
+        rec.l_u_traj[s] = l.u_traj;
+        rec.l_u_cur[s] = l.u_cur;
+      }
+    }
+    int64_t hv_next, hv_steps, lv_next, lv_steps, ha_next, ha_steps, la_next, la_steps;
+    high_next(idx, fin, hvg, hc.value_subgoal_steps, &hv_next, &hv_steps);
+    high_next(idx, fin, hvg, hc.low_subgoal_steps, &lv_next, &lv_steps);
+    high_next(idx, fin, hag, hc.actor_subgoal_steps, &ha_next, &ha_steps);
+    const int64_t la_goal = idx + hc.actor_subgoal_steps < fin ? idx + hc.actor_subgoal_steps : fin;
+    high_next(idx, fin, hag, hc.low_subgoal_steps, &la_next, &la_steps);
+    const int t = threadIdx.x;
+    sel[0][t] = idx;
+    sel[1][t] = next;
+    sel[2][t] = hvg;
+    sel[3][t] = hag;
+    sel[4][t] = hv_next;
+    sel[5][t] = lv_next;
+    sel[6][t] = lvg;
+    sel[7][t] = ha_next;
+    sel[8][t] = la_goal;
+    sel[9][t] = la_next;
+    if (o.idxs) o.idxs[s] = idx;
+    if (o.high_value_goal_idxs) o.high_value_goal_idxs[s] = hvg;
+    if (o.high_actor_goal_idxs) o.high_actor_goal_idxs[s] = hag;
+    if (o.low_value_goal_idxs) o.low_value_goal_idxs[s] = lvg;
+    const double neg = cfg.gc_negative ? 1.0 : 0.0;
+    o.high_value_offsets[s] = hvg - idx;
+    o.high_value_subgoal_steps[s] = hv_steps;
+    o.high_value_masks[s] = hc.hv_mask_table[hv_steps];
+    o.high_value_rewards[s] = hc.hv_reward_table[hv_steps];
+    o.low_value_subgoal_steps[s] = lv_steps;
+    if (hc.has_low_value_goals) {
+      const double ls = idx == lvg ? 1.0 : 0.0;
+      o.low_value_masks[s] = 1.0 - ls;
+      o.low_value_rewards[s] = ls - neg;
+    } else {
+      o.low_value_masks[s] = hc.lv_mask_table[lv_steps];
+      o.low_value_rewards[s] = hc.lv_reward_table[lv_steps];
+    }
+    const double succ = idx == hvg ? 1.0 : 0.0;
+    o.masks[s] = 1.0 - succ;
+    o.rewards[s] = succ - neg;
+    if (rec.gc.pick) {
+      rec.gc.pick[s] = pick;
+      rec.gc.v_pick[s] = v.pick;
+      rec.gc.v_geom[s] = v.geom;
+      rec.gc.v_dist[s] = v.dist;
+      rec.gc.v_u_traj[s] = v.u_traj;
+      rec.gc.v_u_cur[s] = v.u_cur;
+      rec.gc.a_pick[s] = a.pick;
+      rec.gc.a_geom[s] = a.geom;
+      rec.gc.a_dist[s] = a.dist;
+      rec.gc.a_u_traj[s] = a.u_traj;
+      rec.gc.a_u_cur[s] = a.u_cur;
+    }
+  }
+  __syncthreads();
+  for (int c = 0; c < num_cols; ++c) {
+    const ogbx_gc_column& col = cols.c[c];
+    const int64_t* srow = sel[col.select];
+    const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst;
+    if (col.row_bytes % 16 == 0 && align % 16 == 0)
+      copy_rows<uint4>(col, srow, base, n_here);
+    else if (col.row_bytes % 8 == 0 && align % 8 == 0)
+      copy_rows<uint2>(col, srow, base, n_here);
+    else if (col.row_bytes % 4 == 0 && align % 4 == 0)
+      copy_rows<uint32_t>(col, srow, base, n_here);
+    else
+      copy_rows<uint8_t>(col, srow, base, n_here);
+  }
+}
+
 __global__ void traj_end_kernel(const int64_t* __restrict__ term, int64_t nterm, int64_t nrows,
                                 int64_t* __restrict__ out) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -234,6 +378,56 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
                      (uint32_t)call_index, (uint32_t)(call_index >> 32), v_log_q, a_log_q,
                      idxs_out, value_goal_out, actor_goal_out, masks, rewards, rec);
   OGBX_LAUNCHED("gc_sample_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                            const ogbx_hgc_config* hcfg, const ogbx_gc_column* cols,
+                            int32_t num_cols, int64_t batch, int64_t num_batches,
+                            const ogbx_hgc_draws* draws, uint64_t seed, uint64_t call_index,
+                            const ogbx_hgc_outputs* out, const ogbx_hgc_draw_record* record,
+                            void* stream) {
+  OGBX_CHECK(buf && cfg && hcfg && out, OGBX_EINVAL, "ogbx_hgc_sample: null argument");
+  OGBX_CHECK(out->high_value_offsets && out->high_value_subgoal_steps && out->high_value_masks &&
+                 out->high_value_rewards && out->low_value_subgoal_steps && out->low_value_masks &&
+                 out->low_value_rewards && out->masks && out->rewards,
+             OGBX_EINVAL, "ogbx_hgc_sample: missing scalar output");
+  OGBX_CHECK(hcfg->hv_mask_table && hcfg->hv_reward_table && hcfg->lv_mask_table && hcfg->lv_reward_table,
+             OGBX_EINVAL, "ogbx_hgc_sample: missing reward/mask tables");
+  OGBX_CHECK(hcfg->value_subgoal_steps >= 0 && hcfg->low_subgoal_steps >= 0 && hcfg->actor_subgoal_steps >= 0,
+             OGBX_EINVAL, "ogbx_hgc_sample: negative subgoal steps");
+  OGBX_CHECK(!hcfg->has_low_value_goals || (hcfg->low_discount > 0.0 && hcfg->low_discount < 1.0),
+             OGBX_EINVAL, "ogbx_hgc_sample: low_discount must be in (0, 1)");
+  OGBX_CHECK(num_cols >= 0 && num_cols <= kGcMaxCols, OGBX_EINVAL, "ogbx_hgc_sample: at most 32 columns");
+  OGBX_CHECK(batch > 0 && num_batches > 0, OGBX_EINVAL, "batch and num_batches must be > 0");
+  OGBX_CHECK(buf->num_rows > 0 && buf->traj_end, OGBX_EINVAL, "empty trajectory buffer");
+  OGBX_CHECK(buf->valid_idxs == nullptr || buf->num_valid > 0, OGBX_EINVAL,
+             "no valid transitions in the dataset");
+  GcColumns cc{};
+  for (int i = 0; i < num_cols; ++i) {
+    OGBX_CHECK(cols[i].src && cols[i].dst && cols[i].row_bytes > 0 && cols[i].select >= 0 &&
+                   cols[i].select < kHgcSel,
+               OGBX_EINVAL, "ogbx_hgc_sample: bad column descriptor");
+    cc.c[i] = cols[i];
+  }
+  ogbx_hgc_draws dr{};
+  if (draws) dr = *draws;
+  ogbx_hgc_draw_record rec{};
+  if (record) rec = *record;
+  const int64_t total = batch * num_batches;
+  int64_t tile = total / 512;
+  if (tile < 1) tile = 1;
+  if (tile > kGcMaxTile) tile = kGcMaxTile;
+  const int64_t blocks = (total + tile - 1) / tile;
+  uint32_t k0, k1;
+  seed_key(seed, kTagHgcSample, &k0, &k1);
+  const double v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
+  const double a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
+  const double l_log_q = hcfg->has_low_value_goals ? std::log(1.0 - (1.0 - hcfg->low_discount)) : 0.0;
+  hipLaunchKernelGGL(hgc_sample_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, *buf,
+                     *cfg, *hcfg, cc, num_cols, total, (int)tile, dr, k0, k1, (uint32_t)call_index,
+                     (uint32_t)(call_index >> 32), v_log_q, a_log_q, l_log_q, *out, rec);
+  OGBX_LAUNCHED("hgc_sample_kernel");
   return OGBX_OK;
 }
 

@@ -248,8 +248,17 @@ class GCDataset:
         self._seed = int(seed) if seed is not None else None
         self._calls = 0
         self._plain = _plain
+        self._out_cache = {}
+        self._no_draws = GcDraws()
 
     # ---------------------------------------------------------------- helpers
+    def _p_aug_draw(self, out, evaluation):
+        # p_aug draw (datasets.py:278-279): image crops apply only to 4-D arrays
+        p_aug = self.config.get('p_aug')
+        if p_aug is not None and not evaluation:
+            if np.random.rand() < p_aug and any(v.dim() == 4 for v in out.values()):
+                raise NotImplementedError('image augmentation (visual datasets) is out of scope')
+
     def _next_seed(self):
         if self._seed is None:
             self._seed = int(np.random.randint(0, 2**63 - 1))
@@ -281,7 +290,7 @@ class GCDataset:
         return out, cols
 
     def sample(self, batch_size, idxs=None, evaluation=False, draws=None, record_draws=False,
-               num_batches=1, _keys=None):
+               num_batches=1, _keys=None, out=None):
         """GCDataset.sample (datasets.py:213-294), one fused launch.
 
         draws: optional dict of injected reference draws (see ``_DRAW_ORDER``;
@@ -289,9 +298,25 @@ class GCDataset:
         record_draws: also return the draws the kernel used (``out['_draws']``).
         num_batches > 1: sample that many independent batches in the same launch
         (outputs have a leading num_batches*batch_size dimension).
+        out: a batch dict returned by an earlier call with the same batch_size /
+        num_batches (and no idxs/draws/record_draws): its tensors are refilled
+        in place (stream ordered, so consumers enqueued earlier read the old
+        batch) and it is returned.  Skips all per-call allocation.
         """
         torch = _torch()
         total = int(batch_size) * int(num_batches)
+        plain_call = idxs is None and not draws and not record_draws and _keys is None
+        if out is not None and plain_call:
+            hit = self._out_cache.get(id(out))
+            if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
+                _, _, col_arr, ncols, masks, rewards, idx_out = hit
+                seed, call = self._next_seed()
+                _lib.check(self._L.ogbx_gc_sample(
+                    self._buf, self._cfg, ctypes.cast(col_arr, ctypes.c_void_p), ncols, int(batch_size),
+                    int(num_batches), self._no_draws, seed, call, _lib.ptr(idx_out), None, None,
+                    _lib.ptr(masks), _lib.ptr(rewards), None, _lib.stream_of(self.device)), 'gc_sample')
+                self._p_aug_draw(out, evaluation)
+                return out
         out, cols = self._columns(total, _keys)
         col_arr = (GcColumn * max(1, len(cols)))(*cols)
         masks = torch.empty(total, dtype=torch.float64, device=self.device)
@@ -329,17 +354,220 @@ class GCDataset:
             _lib.ptr(rewards), rec, _lib.stream_of(self.device)), 'gc_sample')
         if self._plain:
             out['_idxs'] = idx_out
+        else:
+            out['masks'] = masks
+            out['rewards'] = rewards
+        if plain_call:
+            # remember the descriptors so that sample(..., out=this) skips setup
+            if len(self._out_cache) >= 2:
+                self._out_cache.clear()
+            self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), col_arr, len(cols), masks, rewards,
+                                        idx_out)
+        if self._plain:
             return out
-        out['masks'] = masks
-        out['rewards'] = rewards
-        # p_aug draw (datasets.py:278-279): image crops apply only to 4-D arrays
-        p_aug = self.config.get('p_aug')
-        if p_aug is not None and not evaluation:
-            if np.random.rand() < p_aug and any(v.dim() == 4 for v in out.values()):
-                raise NotImplementedError('image augmentation (visual datasets) is out of scope')
+        self._p_aug_draw(out, evaluation)
         if record_draws:
             out['_draws'] = rec_t
             out['_idxs'] = idx_out
             out['_value_goal_idxs'] = vg
             out['_actor_goal_idxs'] = ag
+        return out
+
+
+# ----------------------------------------------------------------------------- HGCDataset
+
+_HDRAW_LOW = ('l_pick', 'l_geom', 'l_u_traj', 'l_u_cur')
+_HDRAW_INT = _DRAW_INT + ('l_pick', 'l_geom')
+
+
+class HgcConfig(ctypes.Structure):
+    _fields_ = [
+        ('value_subgoal_steps', ctypes.c_int64),
+        ('low_subgoal_steps', ctypes.c_int64),
+        ('actor_subgoal_steps', ctypes.c_int64),
+        ('has_low_value_goals', ctypes.c_int32),
+        ('pad_', ctypes.c_int32),
+        ('low_discount', ctypes.c_double),
+        ('hv_mask_table', ctypes.c_void_p),
+        ('hv_reward_table', ctypes.c_void_p),
+        ('lv_mask_table', ctypes.c_void_p),
+        ('lv_reward_table', ctypes.c_void_p),
+    ]
+
+
+class HgcDraws(ctypes.Structure):
+    _fields_ = [('gc', GcDraws)] + [(k, ctypes.c_void_p) for k in _HDRAW_LOW]
+
+
+class HgcDrawRecord(ctypes.Structure):
+    _fields_ = [('gc', GcDrawRecord)] + [(k, ctypes.c_void_p) for k in _HDRAW_LOW]
+
+
+_HGC_SCALARS = ('idxs', 'high_value_goal_idxs', 'high_actor_goal_idxs', 'low_value_goal_idxs',
+                'high_value_offsets', 'high_value_subgoal_steps', 'high_value_masks', 'high_value_rewards',
+                'low_value_subgoal_steps', 'low_value_masks', 'low_value_rewards', 'masks', 'rewards')
+
+
+class HgcOutputs(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in _HGC_SCALARS]
+
+
+def _bind_hgc():
+    L = _bind()
+    if not getattr(L, '_hgc_bound', False):
+        P = ctypes.POINTER
+        L.ogbx_hgc_sample.restype = ctypes.c_int32
+        L.ogbx_hgc_sample.argtypes = [
+            P(GcBuffer), P(GcConfig), P(HgcConfig), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+            ctypes.c_int64, P(HgcDraws), ctypes.c_uint64, ctypes.c_uint64, P(HgcOutputs), P(HgcDrawRecord),
+            ctypes.c_void_p,
+        ]
+        L._hgc_bound = True
+    return L
+
+
+def _subgoal_tables(discount, K, gc_negative, device):
+    """masks / rewards of HGCDataset.sample as functions of the clipped subgoal
+    step count s in [0, K] (datasets.py:533-541, 550-556), computed with the
+    reference's own float64 NumPy expressions so the device lookup is bit-exact."""
+    torch = _torch()
+    s = np.arange(K + 1, dtype=np.int64)
+    succ = (s < K).astype(float)
+    masks = 1.0 - succ
+    rewards = -(1 - discount ** s) / (1 - discount) if gc_negative else (discount ** s) * succ
+    return (torch.as_tensor(np.ascontiguousarray(masks), device=device),
+            torch.as_tensor(np.ascontiguousarray(rewards, dtype=np.float64), device=device))
+
+
+class HGCDataset(GCDataset):
+    """Hierarchical goal-conditioned sampler (reference: datasets.py:467-643).
+
+    Extra config keys (as the reference): subgoal_steps, optional
+    high_subgoal_steps, value_subgoal_steps, actor_subgoal_steps,
+    low_subgoal_steps, low_discount.  One fused launch of hgc_sample_kernel
+    per sample() returns the reference's 27 (28 with low_discount) keys.
+    """
+
+    def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None):
+        super().__init__(dataset, config, preprocess_frame_stack=preprocess_frame_stack, seed=seed)
+        c = config
+        high = c.get('high_subgoal_steps', c['subgoal_steps'])
+        self.value_subgoal_steps = int(high if c.get('value_subgoal_steps') is None else c['value_subgoal_steps'])
+        self.actor_subgoal_steps = int(high if c.get('actor_subgoal_steps') is None else c['actor_subgoal_steps'])
+        self.low_subgoal_steps = int(c.get('low_subgoal_steps', c['subgoal_steps']))
+        self._has_low = c.get('low_discount') is not None
+        dev = self.device
+        self._hv_tab = _subgoal_tables(c['discount'], self.value_subgoal_steps, c['gc_negative'], dev)
+        self._lv_tab = _subgoal_tables(c['discount'], self.low_subgoal_steps, c['gc_negative'], dev)
+        self._hcfg = HgcConfig(
+            self.value_subgoal_steps, self.low_subgoal_steps, self.actor_subgoal_steps, int(self._has_low), 0,
+            float(c['low_discount']) if self._has_low else 0.0,
+            self._hv_tab[0].data_ptr(), self._hv_tab[1].data_ptr(),
+            self._lv_tab[0].data_ptr(), self._lv_tab[1].data_ptr(),
+        )
+        self._Lh = _bind_hgc()
+
+    def _hcolumns(self, total):
+        """Output tensors in the reference's key order, and column descriptors."""
+        torch = _torch()
+        ds = self.dataset
+        out, cols = {}, []
+        goal_src = 'oracle_reps' if 'oracle_reps' in ds else 'observations'
+
+        def col(src_key, select):
+            src = ds[src_key]
+            dst = torch.empty((total,) + tuple(src.shape[1:]), dtype=src.dtype, device=self.device)
+            row_bytes = src[0].numel() * src.element_size() if src.dim() > 1 else src.element_size()
+            cols.append(GcColumn(src.data_ptr(), dst.data_ptr(), row_bytes, select, 0))
+            return dst
+
+        def scalar(dtype):
+            return torch.empty(total, dtype=dtype, device=self.device)
+
+        for k in ds.keys():
+            out[k] = col(k, 0)
+        if 'next_observations' not in ds:
+            out['next_observations'] = col('observations', 1)
+        i64, f64 = torch.int64, torch.float64
+        out['high_value_reps'] = out['observations']
+        out['high_value_goals'] = col(goal_src, 2)
+        out['high_value_actions'] = col(goal_src, 4)
+        out['high_value_next_observations'] = col('observations', 4)
+        for k, dt in (('high_value_offsets', i64), ('high_value_subgoal_steps', i64), ('high_value_masks', f64),
+                      ('high_value_rewards', f64)):
+            out[k] = scalar(dt)
+        out['low_value_next_observations'] = col('observations', 5)
+        for k, dt in (('low_value_subgoal_steps', i64), ('low_value_masks', f64), ('low_value_rewards', f64)):
+            out[k] = scalar(dt)
+        if self._has_low:
+            out['low_value_goals'] = col(goal_src, 6)
+        out['value_goals'] = out['high_value_goals']
+        out['masks'] = scalar(f64)
+        out['rewards'] = scalar(f64)
+        out['high_actor_goals'] = col(goal_src, 3)
+        out['high_actor_actions'] = col(goal_src, 7)
+        out['high_actor_next_observations'] = col('observations', 7)
+        out['high_actor_targets'] = out['high_actor_actions']
+        out['low_actor_goals'] = col(goal_src, 8)
+        out['low_actor_goal_observations'] = col('observations', 8)
+        out['low_actor_next_observations'] = col('observations', 9)
+        return out, cols
+
+    def sample(self, batch_size, idxs=None, evaluation=False, draws=None, record_draws=False, num_batches=1,
+               out=None):
+        """HGCDataset.sample (datasets.py:496-643), one fused launch.  Arguments
+        as GCDataset.sample; draws may also carry the low-level l_* draws."""
+        torch = _torch()
+        total = int(batch_size) * int(num_batches)
+        plain_call = idxs is None and not draws and not record_draws
+        hit = self._out_cache.get(id(out)) if (out is not None and plain_call) else None
+        if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
+            _, _, col_arr, ncols, outs = hit
+            dr, rec, keep = HgcDraws(), None, []
+        else:
+            out, cols = self._hcolumns(total)
+            col_arr = (GcColumn * max(1, len(cols)))(*cols)
+            ncols = len(cols)
+            ptr = lambda k: out[k].data_ptr() if k in out else None  # noqa: E731
+            outs = HgcOutputs(None, None, None, None, *[ptr(k) for k in _HGC_SCALARS[4:]])
+            keep = []
+            dr = HgcDraws()
+            if idxs is not None:
+                t = _to_device(idxs, self.device).to(torch.int64).reshape(-1)
+                assert t.numel() == total
+                keep.append(t)
+                dr.gc.idxs = t.data_ptr()
+            for k, v in (draws or {}).items():
+                if k == 'idxs':
+                    continue
+                t = _to_device(v, self.device).to(torch.int64 if k in _HDRAW_INT else torch.float64).reshape(-1)
+                assert t.numel() == total, k
+                keep.append(t)
+                setattr(dr.gc if hasattr(dr.gc, k) else dr, k, t.data_ptr())
+            rec = None
+            if record_draws:
+                rec_t = {k: torch.empty(total, dtype=torch.int64 if k in _HDRAW_INT else torch.float64,
+                                        device=self.device) for k in _DRAW_ORDER + _HDRAW_LOW}
+                rec = HgcDrawRecord(GcDrawRecord(*[rec_t[k].data_ptr() for k in _DRAW_ORDER]),
+                                    *[rec_t[k].data_ptr() for k in _HDRAW_LOW])
+                idx_t = {k: torch.empty(total, dtype=torch.int64, device=self.device) for k in _HGC_SCALARS[:4]}
+                for k, t in idx_t.items():
+                    setattr(outs, k, t.data_ptr())
+            if plain_call:
+                if len(self._out_cache) >= 2:
+                    self._out_cache.clear()
+                self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), col_arr, ncols, outs)
+        seed, call = self._next_seed()
+        _lib.check(self._Lh.ogbx_hgc_sample(
+            self._buf, self._cfg, self._hcfg, ctypes.cast(col_arr, ctypes.c_void_p), ncols, int(batch_size),
+            int(num_batches), dr, seed, call, outs, rec, _lib.stream_of(self.device)), 'hgc_sample')
+        self._p_aug_draw(out, evaluation)
+        if record_draws:
+            out['_draws'] = rec_t
+            for k, t in idx_t.items():
+                out['_' + k] = t
+            if not self._has_low:
+                for k in _HDRAW_LOW:
+                    out['_draws'].pop(k)
+        del keep
         return out

@@ -78,3 +78,84 @@ def sample(data, cfg, draws, idxs=None):
     out['masks'] = 1.0 - s
     out['rewards'] = s - (1.0 if cfg['gc_negative'] else 0.0)
     return out, idxs, vg, ag
+
+
+def compute_high_next_idxs(idxs, fin, goal, steps):
+    """HGCDataset.compute_high_next_idxs (impls/utils/datasets.py:478-491)."""
+    s = np.minimum(np.full(len(idxs), steps, np.int64), fin - idxs)
+    diff = goal - idxs
+    s = np.where((0 <= diff) & (diff < s), diff, s)
+    return idxs + s, s
+
+
+def hgc_sample(data, cfg, draws):
+    """One HGCDataset.sample (impls/utils/datasets.py:496-643) with the given
+    draws (pick, v_*, [l_*], a_*).  Returns the batch dict (reference keys and
+    order) and the goal indices."""
+    size = max(len(v) for v in data.values())
+    valid = np.nonzero(data['valids'] > 0)[0] if 'valids' in data else None
+    idxs = (valid[draws['pick']] if valid is not None else draws['pick']).astype(np.int64)
+    fin = traj_end(data['terminals'])[idxs]
+
+    def goals(p, p_cur, p_traj, geom):
+        rnd = valid[draws[p + 'pick']] if valid is not None else draws[p + 'pick']
+        if geom:
+            traj = np.minimum(idxs + draws[p + 'geom'], fin)
+        else:
+            d = draws[p + 'dist']
+            traj = np.round(np.minimum(idxs + 1, fin) * d + fin * (1 - d)).astype(np.int64)
+        if p_cur == 1.0:
+            return idxs
+        g = np.where(draws[p + 'u_traj'] < p_traj / (1.0 - p_cur), traj, rnd)
+        return np.where(draws[p + 'u_cur'] < p_cur, idxs, g)
+
+    obs = data['observations']
+    src = data['oracle_reps'] if 'oracle_reps' in data else obs
+    disc = cfg['discount']
+    out = {k: v[idxs] for k, v in data.items()}
+    if 'next_observations' not in data:
+        out['next_observations'] = obs[np.minimum(idxs + 1, size - 1)]
+    hvg = goals('v_', cfg['value_p_curgoal'], cfg['value_p_trajgoal'], cfg['value_geom_sample'])
+    high = cfg.get('high_subgoal_steps', cfg['subgoal_steps'])
+    vsteps = high if cfg.get('value_subgoal_steps') is None else cfg['value_subgoal_steps']
+    hv_next, hv_s = compute_high_next_idxs(idxs, fin, hvg, vsteps)
+    out['high_value_reps'] = out['observations']
+    out['high_value_goals'] = src[hvg]
+    out['high_value_actions'] = src[hv_next]
+    out['high_value_next_observations'] = obs[hv_next]
+    out['high_value_offsets'] = hvg - idxs
+    succ = (hv_s < vsteps).astype(float)
+    out['high_value_subgoal_steps'] = hv_s
+    out['high_value_masks'] = 1.0 - succ
+    out['high_value_rewards'] = (-(1 - disc ** hv_s) / (1 - disc) if cfg['gc_negative'] else (disc ** hv_s) * succ)
+    lsteps = cfg.get('low_subgoal_steps', cfg['subgoal_steps'])
+    lv_next, lv_s = compute_high_next_idxs(idxs, fin, hvg, lsteps)
+    out['low_value_next_observations'] = obs[lv_next]
+    succ = (lv_s < lsteps).astype(float)
+    out['low_value_subgoal_steps'] = lv_s
+    out['low_value_masks'] = 1.0 - succ
+    out['low_value_rewards'] = (-(1 - disc ** lv_s) / (1 - disc) if cfg['gc_negative'] else (disc ** lv_s) * succ)
+    lvg = None
+    if cfg.get('low_discount') is not None:
+        lvg = goals('l_', cfg['value_p_curgoal'], cfg['value_p_trajgoal'], True)
+        out['low_value_goals'] = src[lvg]
+        s = (idxs == lvg).astype(float)
+        out['low_value_masks'] = 1.0 - s
+        out['low_value_rewards'] = s - (1.0 if cfg['gc_negative'] else 0.0)
+    s = (idxs == hvg).astype(float)
+    out['value_goals'] = out['high_value_goals']
+    out['masks'] = 1.0 - s
+    out['rewards'] = s - (1.0 if cfg['gc_negative'] else 0.0)
+    hag = goals('a_', cfg['actor_p_curgoal'], cfg['actor_p_trajgoal'], cfg['actor_geom_sample'])
+    asteps = high if cfg.get('actor_subgoal_steps') is None else cfg['actor_subgoal_steps']
+    ha_next, _ = compute_high_next_idxs(idxs, fin, hag, asteps)
+    out['high_actor_goals'] = src[hag]
+    out['high_actor_actions'] = src[ha_next]
+    out['high_actor_next_observations'] = obs[ha_next]
+    out['high_actor_targets'] = out['high_actor_actions']
+    la_goal = np.minimum(idxs + asteps, fin)
+    out['low_actor_goals'] = src[la_goal]
+    out['low_actor_goal_observations'] = obs[la_goal]
+    la_next, _ = compute_high_next_idxs(idxs, fin, hag, lsteps)
+    out['low_actor_next_observations'] = obs[la_next]
+    return out, dict(idxs=idxs, hvg=hvg, hag=hag, lvg=lvg)

@@ -212,6 +212,8 @@ def main():
             ns = {'__name__': extra, '__file__': path}
             exec(compile(open(path).read(), path, 'exec'), ns)
             ns['main']()
+            if 'main_hgc' in ns:
+                ns['main_hgc']()
 
 
 if __name__ == '__main__':

@@ -243,5 +243,95 @@ def main():
     print('gc golden:', len(out), 'arrays')
 
 
+HGC_CONFIGS = {
+    # HIQL-style (impls/agents/hiql.py defaults; subgoal_steps shortened for short trajectories)
+    'hiql': dict(discount=0.99, value_p_curgoal=0.2, value_p_trajgoal=0.5, value_p_randomgoal=0.3,
+                 value_geom_sample=True, actor_p_curgoal=0.0, actor_p_trajgoal=1.0, actor_p_randomgoal=0.0,
+                 actor_geom_sample=False, gc_negative=True, p_aug=0.0, frame_stack=None, subgoal_steps=10),
+    # separate value/actor/low subgoal steps, low-level value goals, positive rewards
+    'hlow': dict(discount=0.97, value_p_curgoal=0.3, value_p_trajgoal=0.4, value_p_randomgoal=0.3,
+                 value_geom_sample=False, actor_p_curgoal=0.2, actor_p_trajgoal=0.5, actor_p_randomgoal=0.3,
+                 actor_geom_sample=True, gc_negative=False, p_aug=None, frame_stack=None, subgoal_steps=6,
+                 value_subgoal_steps=7, actor_subgoal_steps=4, low_subgoal_steps=3, low_discount=0.95),
+    # current-state value goals (no u draws), high_subgoal_steps override
+    'hcur': dict(discount=0.9, value_p_curgoal=1.0, value_p_trajgoal=0.0, value_p_randomgoal=0.0,
+                 value_geom_sample=True, actor_p_curgoal=0.0, actor_p_trajgoal=0.5, actor_p_randomgoal=0.5,
+                 actor_geom_sample=False, gc_negative=True, p_aug=None, frame_stack=None, subgoal_steps=5,
+                 high_subgoal_steps=12, low_discount=0.9),
+}
+
+
+def hgc_draws_from_log(log, B, cfg):
+    """Map the np.random call log of one HGCDataset.sample (datasets.py:496-643)
+    to named draws: pick, v_*, [l_*], a_* (same layout as ogbx_hgc_draws)."""
+    it = iter(log)
+    d = {}
+    name, v = next(it)
+    assert name == 'randint'
+    d['pick'] = v.astype(np.int64)
+
+    def goal(p, p_cur, geom):
+        name, v = next(it)
+        assert name == 'randint'
+        d[p + 'pick'] = v.astype(np.int64)
+        name, v = next(it)
+        if geom:
+            assert name == 'geometric'
+            d[p + 'geom'] = v.astype(np.int64)
+            d[p + 'dist'] = np.zeros(B)
+        else:
+            assert name == 'rand'
+            d[p + 'dist'] = v.astype(np.float64)
+            d[p + 'geom'] = np.zeros(B, np.int64)
+        if p_cur == 1.0:
+            d[p + 'u_traj'] = np.ones(B)
+            d[p + 'u_cur'] = np.zeros(B)
+        else:
+            for k in ('u_traj', 'u_cur'):
+                name, v = next(it)
+                assert name == 'rand'
+                d[p + k] = v.astype(np.float64)
+
+    goal('v_', cfg['value_p_curgoal'], cfg['value_geom_sample'])
+    if cfg.get('low_discount') is not None:
+        goal('l_', cfg['value_p_curgoal'], True)
+    goal('a_', cfg['actor_p_curgoal'], cfg['actor_geom_sample'])
+    return d
+
+
+def main_hgc():
+    utils, dsm, _ = reference_modules()
+    rng = np.random.RandomState(4321)
+    out = {}
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, 'synth.npz')
+        synthetic_npz(path, rng, n_traj=41, ob_dim=4, act_dim=2, min_len=2, max_len=30)
+        raw = dict(np.load(path))
+        for k, v in raw.items():
+            out[f'raw_{k}'] = v
+        d = utils.load_dataset(path, compact_dataset=True, add_info=False)
+        for cname, cfg in HGC_CONFIGS.items():
+            for oracle in (False, True):
+                data = dict(d)
+                if oracle:
+                    data['oracle_reps'] = raw['qpos'][: len(data['observations'])].astype(np.float32)
+                hgc = dsm.HGCDataset(dsm.Dataset.create(**data), dict(cfg))
+                tag = f'{cname}_{"oracle" if oracle else "obs"}'
+                B = 301
+                np.random.seed(sum(map(ord, tag)) + 11)
+                with Recorder() as rec:
+                    batch = hgc.sample(B)
+                for k, v in hgc_draws_from_log(rec.log, B, cfg).items():
+                    out[f'hgc_{tag}_draw_{k}'] = v
+                for k, v in batch.items():
+                    out[f'hgc_{tag}_out_{k}'] = np.asarray(v)
+                out[f'hgc_{tag}_keys'] = np.array(list(batch.keys()))
+    np.savez_compressed(os.path.join(OUT, 'hgc_golden.npz'), **out)
+    print('hgc golden:', len(out), 'arrays')
+
+
 if __name__ == '__main__':
     main()
+    main_hgc()

@@ -154,3 +154,22 @@ def test_humanoid_scale_properties(gpu):
     assert torch.equal(out['actions'], ds['actions'][idx])
     assert bool((valids[idx] == 1).all())
     assert bool(((ag // L) == (idx // L)).all())
+
+
+def test_out_reuse_matches_fresh_calls(gpu, gold):
+    """sample(B, out=prev) refills prev in place with exactly the batch a fresh
+    call would return (same seed, same call index)."""
+    data = orc.load_dataset(_raw(gold), compact_dataset=True)
+    cfg = dict(CONFIGS['gciql'] if 'gciql' in CONFIGS else next(iter(CONFIGS.values())), p_aug=None, frame_stack=None)
+    g1 = GCDataset(Dataset(data, device=gpu), cfg, seed=7)
+    g2 = GCDataset(Dataset(data, device=gpu), cfg, seed=7)
+    a1 = {k: v.clone() for k, v in g1.sample(256).items()}
+    b1 = g1.sample(256)
+    a2 = g2.sample(256)
+    for k in a1:
+        assert torch.equal(a1[k], a2[k]), k
+    ptrs = {k: v.data_ptr() for k, v in a2.items()}
+    b2 = g2.sample(256, out=a2)
+    assert b2 is a2 and all(v.data_ptr() == ptrs[k] for k, v in b2.items())
+    for k in b1:
+        assert torch.equal(b1[k], b2[k]), k
