@@ -348,6 +348,98 @@ def bench_gcsample(args, world, rank, dev):
     return result
 
 
+def bench_hgcsample(args, world, rank, dev):
+    """HGCDataset.sample(1024) on the same 1M-row humanoid buffer with the HIQL
+    humanoidmaze config (discount 0.995, subgoal_steps 100; impls/hyperparameters.sh).
+    A step = one sample(1024) refilling the previous batch (one fused launch)."""
+    from ogbench_amd.datasets import Dataset, HGCDataset
+
+    n_traj, L = 500, 2000
+    R = n_traj * L
+    g = torch.Generator(device=dev)
+    g.manual_seed(3 + rank)
+    term = torch.zeros(R, device=dev)
+    term[L - 1 :: L] = 1
+    data = dict(
+        observations=torch.randn(R, 69, device=dev, generator=g),
+        actions=torch.rand(R, 21, device=dev, generator=g) * 2 - 1,
+        terminals=torch.clamp(term + torch.cat([term[1:], torch.ones(1, device=dev)]), max=1.0),
+        valids=1.0 - term,
+    )
+    cfg = dict(discount=0.995, value_p_curgoal=0.2, value_p_trajgoal=0.5, value_p_randomgoal=0.3,
+               value_geom_sample=True, actor_p_curgoal=0.0, actor_p_trajgoal=1.0, actor_p_randomgoal=0.0,
+               actor_geom_sample=False, gc_negative=True, p_aug=0.0, frame_stack=None, subgoal_steps=100)
+    hgc = HGCDataset(Dataset(data, device=dev), cfg, seed=rank)
+    B = 1024
+    batch = hgc.sample(B)
+
+    def step(i):
+        hgc.sample(B, out=batch)
+
+    for i in range(args.warmup):
+        step(i)
+    dt = _timed(step, args.steps, world, dev)
+    kern_ms = _per_launch_ms(step, min(args.steps, 200), dev)
+    # DESIGN.md: 12 gathered 276-B observation rows + actions 84 + terminals/valids 8,
+    # read and written, + valid_idxs/traj_end lookups 16 + 9 x 8-B scalars written
+    per_sample = 2 * (12 * 276 + 84 + 8) + 16 + 72
+    achieved = per_sample * B / (kern_ms * 1e-3) / 1e9
+    extra = {}
+    if not args.no_extras:
+        NB = 128
+        big = hgc.sample(B, num_batches=NB)
+
+        def fused(i):
+            hgc.sample(B, num_batches=NB, out=big)
+
+        reps = max(1, args.steps // 32)
+        fdt = _timed(fused, reps, world, dev)
+        fk_ms = _per_launch_ms(fused, 5, dev)
+        extra = dict(fused_128x1024_samples_per_s=B * NB * reps * world / fdt, fused_128x1024_kernel_ms=fk_ms,
+                     fused_128x1024_achieved_GBs=per_sample * B * NB / (fk_ms * 1e-3) / 1e9)
+    result = dict(
+        metric='HGCDataset.sample samples/sec, humanoidmaze-large-navigate-v0 1M-row buffer, batch 1024',
+        value=B * args.steps * world / dt, unit='samples/s', n_gpus=world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=dt / args.steps * 1e3, higher_is_better=True, scaling='weak', vs_baseline=None,
+        dtype='f32', data='synthetic (N(0,1) obs, U[-1,1] actions; 500 x 2000-row trajectories)',
+        config=dict(workload='humanoidmaze-large-navigate-v0 offline replay (HIQL sampler)', rows=R, batch=B,
+                    agent_config='hiql humanoid (discount 0.995, subgoal_steps 100)',
+                    parallelism=f'replica x{world}'),
+        roofline=dict(bound='hbm', kernel='hgc_sample_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('hgc_sample_kernel', kern_ms),
+                      kernel_ms=kern_ms, alg_bytes_per_launch=per_sample * B),
+        extra=extra,
+    )
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline_hgc(data, cfg, B, args)
+    return result
+
+
+def cpu_baseline_hgc(data, cfg, B, args):
+    """The NumPy oracle restatement of HGCDataset.sample (kind 'port', 1 core)."""
+    from oracle import gcdataset_np as orc
+
+    host = {k: v.cpu().numpy() for k, v in data.items()}
+    nvalid = int((host['valids'] > 0).sum())
+    rng = np.random.RandomState(0)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        d = dict(pick=rng.randint(nvalid, size=B))
+        for p, geom in (('v_', True), ('a_', False)):
+            d[p + 'pick'] = rng.randint(nvalid, size=B)
+            if geom:
+                d[p + 'geom'] = rng.geometric(1 - cfg['discount'], size=B)
+            else:
+                d[p + 'dist'] = rng.rand(B)
+            d[p + 'u_traj'] = rng.rand(B)
+            d[p + 'u_cur'] = rng.rand(B)
+        orc.hgc_sample(host, cfg, d)
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n * B / dt, unit='samples/s', cores=1, kind='port',
+                sample=f'{n} batches of {B} on the 1M-row humanoid buffer ({dt:.1f} s)')
+
+
 def cpu_baseline_gc(data, cfg, B, args):
     """The NumPy oracle restatement of GCDataset.sample (kind 'port', 1 core),
     with np.random draws in the reference's call order, on the same buffer."""
@@ -467,7 +559,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=100)
-    ap.add_argument('--workload', default='pointmaze', choices=['pointmaze', 'powder', 'gcsample'])
+    ap.add_argument('--workload', default='pointmaze', choices=['pointmaze', 'powder', 'gcsample', 'hgcsample'])
     ap.add_argument('--num-envs', type=int, default=65536)
     ap.add_argument('--ring', type=int, default=128)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -483,7 +575,7 @@ def main():
     import sys
 
     sys.path.insert(0, ROOT)
-    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, gcsample=bench_gcsample)[args.workload]
+    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, gcsample=bench_gcsample, hgcsample=bench_hgcsample)[args.workload]
     result = fn(args, world, rank, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
