@@ -397,6 +397,32 @@ ogbx_status ogbx_powder_forward(ogbx_powder_t env, const uint8_t* world_in, int6
                                 int32_t steps, uint8_t* world_out, void* stream);
 
 /* ======================================================================
+ * Dataset loader and relabel pass (ogbench/utils.py:14-96,
+ * ogbench/relabel_utils.py).  Device buffers; rows are dense.
+ * ====================================================================== */
+
+/* Compact-dataset rewrite of the raw terminals t[n] (utils.py:65-76):
+ * valids = 1 - t, shifted = t[i+1] (1.0 past the end),
+ * terminals = min(t + shifted, 1).  Any output may be NULL. */
+ogbx_status ogbx_compact_terminals(const float* terminals_in, int64_t n, float* terminals_out,
+                                   float* valids_out, float* shifted_out, void* stream);
+
+/* dst[k] = src[idx[k]] for rows of row_bytes bytes (k < n).  With idx from
+ * ogbx_nonzero_f32 this is the regular-dataset mask compaction
+ * (utils.py:77-94: observations[ob_mask], observations[next_ob_mask], ...). */
+ogbx_status ogbx_gather_rows(const void* src, int64_t row_bytes, const int64_t* idx, int64_t n, void* dst,
+                             void* stream);
+
+/* Maze branch of relabel_dataset + add_oracle_reps in one pass over qpos
+ * (float32 or float64 [num_rows, qpos_stride]): success = ||qpos[:,0:2] -
+ * goal|| <= goal_tol in float64; rewards = success - 1, masks = 1 - success
+ * (float32 [num_rows]); oracle_reps = float32(qpos[:, 0:2]) ([num_rows, 2]).
+ * Any output may be NULL.  relabel_utils.py:17-31,116-127,166. */
+ogbx_status ogbx_relabel_maze(const void* qpos, int32_t qpos_is_f64, int64_t num_rows, int64_t qpos_stride,
+                              double goal_x, double goal_y, double goal_tol, float* rewards, float* masks,
+                              float* oracle_reps, void* stream);
+
+/* ======================================================================
  * Evaluation counters (impls/utils/evaluation.py:36-123, impls/main.py:226-258)
  * ====================================================================== */
 

@@ -212,8 +212,9 @@ def main():
             ns = {'__name__': extra, '__file__': path}
             exec(compile(open(path).read(), path, 'exec'), ns)
             ns['main']()
-            if 'main_hgc' in ns:
-                ns['main_hgc']()
+            for fn in ('main_hgc', 'main_relabel', 'main_names'):
+                if fn in ns:
+                    ns[fn]()
 
 
 if __name__ == '__main__':

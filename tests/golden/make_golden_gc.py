@@ -332,6 +332,91 @@ def main_hgc():
     print('hgc golden:', len(out), 'arrays')
 
 
+def main_relabel():
+    """relabel_dataset / add_oracle_reps (maze branch) of the reference
+    ogbench/relabel_utils.py with a stand-in env (the attributes they read)."""
+    _, _, relabel = reference_modules()
+    rng = np.random.RandomState(99)
+    out = {}
+
+    class _Unwrapped:
+        _reward_task_id = 2
+        _goal_tol = 1.0
+
+    class _Env:
+        unwrapped = _Unwrapped()
+
+        def reset(self):
+            return None
+
+    for qdt in ('f32', 'f64'):
+        n = 5000
+        goal = np.array([28.0, 16.0])
+        q = np.concatenate([rng.uniform(-4, 40, (n, 2)), rng.normal(size=(n, 13))], 1)
+        # exact-boundary rows: distance exactly 1.0 and one ulp around it
+        q[:4, 0] = goal[0] + np.array([1.0, np.nextafter(1.0, 2), np.nextafter(1.0, 0), 0.6])
+        q[:4, 1] = goal[1] + np.array([0.0, 0.0, 0.0, 0.8])
+        q[4:200, :2] = goal + rng.uniform(-1.2, 1.2, (196, 2))
+        q = q.astype(np.float32 if qdt == 'f32' else np.float64)
+        env = _Env()
+        env.unwrapped.cur_goal_xy = goal
+        ds = dict(qpos=q.copy())
+        relabel.relabel_dataset('pointmaze-large-singletask-task2-v0', env, ds)
+        relabel.add_oracle_reps('pointmaze-large-oraclerep-v0', env, ds)
+        out[f'{qdt}_qpos'] = q
+        out[f'{qdt}_goal'] = goal
+        for k in ('rewards', 'masks', 'oracle_reps'):
+            out[f'{qdt}_{k}'] = ds[k]
+    np.savez_compressed(os.path.join(OUT, 'relabel_golden.npz'), **out)
+    print('relabel golden:', len(out), 'arrays')
+
+
+NAME_CASES = [
+    'pointmaze-large-navigate-v0', 'pointmaze-medium-stitch-v0', 'antmaze-giant-explore-v0',
+    'humanoidmaze-large-navigate-v0', 'pointmaze-large-navigate-singletask-v0',
+    'pointmaze-large-navigate-singletask-task2-v0', 'antmaze-teleport-stitch-singletask-task5-v0',
+    'pointmaze-large-navigate-oraclerep-v0', 'antmaze-medium-navigate-oraclerep-v0', 'powderworld-easy-play-v0',
+    'visual-antmaze-large-navigate-v0',
+]
+
+
+def main_names():
+    """make_env_and_datasets' name grammar (utils.py:160-182), recorded from the
+    reference with gymnasium.make and download_datasets replaced by recorders."""
+    import json
+
+    utils, _, _ = reference_modules()
+    rec = {}
+
+    def fake_make(name, **kw):
+        rec['env_name'], rec['env_kwargs'] = name, kw
+        return object()
+
+    class _Stop(Exception):
+        pass
+
+    def fake_download(names, dataset_dir=None):
+        rec['file_name'] = names[0]
+        raise _Stop()
+
+    utils.gymnasium.make = fake_make
+    utils.download_datasets = fake_download
+    out = []
+    for name in NAME_CASES:
+        rec.clear()
+        try:
+            utils.make_env_and_datasets(name, dataset_dir='/nonexistent')
+        except _Stop:
+            pass
+        out.append(dict(dataset_name=name, env_name=rec['env_name'], env_kwargs=rec['env_kwargs'],
+                        file_name=rec['file_name']))
+    with open(os.path.join(OUT, 'names_golden.json'), 'w') as f:
+        json.dump(out, f, indent=1)
+    print('names golden:', len(out))
+
+
 if __name__ == '__main__':
     main()
     main_hgc()
+    main_relabel()
+    main_names()
