@@ -166,6 +166,24 @@ ogbx_status ogbx_maze_oracle_subgoal(ogbx_maze_t env, const double* start_xy,
                                      const double* goal_xy, int64_t n, double* subgoal_xy,
                                      void* stream);
 
+/* Point-maze expert action of data_gen_scripts/generate_locomaze.py:147-166
+ * (+ the point actor, :44-46): dir = (subgoal - xy) / (||subgoal - xy|| +
+ * 1e-6), action = clip(dir + normal, -1, 1), float64 [n,2].  start_xy /
+ * goal_xy: device f64 [n,2], or both NULL to use the env's own qpos / goal
+ * (then n must be the batch size).  normal: device f64 [n,2] draws of
+ * np.random.normal(0, noise) (injected) or NULL = noise * Box-Muller(Philox
+ * keyed by seed, counted by (row, call_index)). */
+ogbx_status ogbx_maze_expert_action(ogbx_maze_t env, const double* start_xy, const double* goal_xy, int64_t n,
+                                   double noise, const double* normal, uint64_t seed, uint64_t call_index,
+                                   double* action, void* stream);
+
+/* MazeEnv.set_goal(goal_ij) (maze.py:492-501) for the envs with mask != 0
+ * (mask NULL = all): goal = ij_to_xy(goal_ij) plus, if add_noise_to_goal, the
+ * add_noise draws (device f64 [N,2] uniform(-1,1) injected, or NULL = Philox).
+ * goal_ij: device int32 [N,2].  Used by the 'navigate' data collection. */
+ogbx_status ogbx_maze_set_goal(ogbx_maze_t env, const int32_t* goal_ij, const uint8_t* mask, const double* noise,
+                               uint64_t seed, uint64_t call_index, void* stream);
+
 
 /* ======================================================================
  * Offline replay: fused index-gather + hindsight goal relabel

@@ -13,5 +13,7 @@ All compute runs in libogbx.so (HIP, gfx950); there is no CPU fallback.
 from .locomaze import MazeEnv, parse_env_id
 from .powderworld import PowderworldEnv
 from .registry import make, registered_env_ids
+from .utils import load_dataset, make_env_and_datasets
 
-__all__ = ['MazeEnv', 'PowderworldEnv', 'make', 'parse_env_id', 'registered_env_ids']
+__all__ = ['MazeEnv', 'PowderworldEnv', 'load_dataset', 'make', 'make_env_and_datasets', 'parse_env_id',
+           'registered_env_ids']

@@ -81,6 +81,10 @@ _SIGNATURES = {
     'ogbx_maze_xy_to_ij': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     'ogbx_maze_ij_to_xy': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     'ogbx_maze_oracle_subgoal': (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    'ogbx_maze_expert_action': (
+        c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_double, c_void_p, c_uint64, c_uint64, c_void_p, c_void_p]
+    ),
+    'ogbx_maze_set_goal': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_uint64, c_void_p]),
     # powderworld
     'ogbx_powder_create': (c_int32, [P(PowderOpts), c_int64, c_int32, P(c_void_p)]),
     'ogbx_powder_destroy': (c_int32, [c_void_p]),

@@ -87,6 +87,8 @@ __host__ __device__ inline uint32_t bounded_u32(uint32_t w, uint32_t n) {
 enum StreamTag : uint32_t {
   kTagMazeReset = 0x4D5A0001u,
   kTagMazeTeleport = 0x4D5A0002u,
+  kTagMazeExpert = 0x4D5A0003u,
+  kTagMazeGoal = 0x4D5A0004u,
   kTagPowderReset = 0x50570001u,
   kTagPowderAction = 0x50570002u,
   kTagGcSample = 0x47430001u,

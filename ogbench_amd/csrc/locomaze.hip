@@ -330,33 +330,107 @@ __device__ inline int clamp_idx(double f, int hi) {
 }
 
 // get_oracle_subgoal (maze.py:503-550) from the precomputed BFS table.
-__global__ void oracle_subgoal_kernel(const MazeParams* __restrict__ Pp, const int16_t* bfs, const double* start_xy,
-                                      const double* goal_xy, int64_t n, double* sub_xy) {
-  const MazeParams& P = *Pp;
-  const PointModel pm = P.pm;
-  __shared__ uint8_t wall_s[kMaxCells];
-  stage_wall(P, wall_s);
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+// get_oracle_subgoal (maze.py:503-550) for one (start, goal) pair from the
+// precomputed BFS distance table (int16 [goal cell][cell], -1 unreachable).
+__device__ inline void subgoal_of(const MazeParams& P, const uint8_t* wall_s, const int16_t* bfs, double x,
+                                  double y, double gx, double gy, double* sx_out, double* sy_out) {
   const int H = P.H, W = P.W;
-  int si = clamp_idx((start_xy[2 * t + 1] + P.pm.off_y + 0.5 * P.pm.unit) / P.pm.unit, H);
-  int sj = clamp_idx((start_xy[2 * t] + P.pm.off_x + 0.5 * P.pm.unit) / P.pm.unit, W);
-  int gi = clamp_idx((goal_xy[2 * t + 1] + P.pm.off_y + 0.5 * P.pm.unit) / P.pm.unit, H);
-  int gj = clamp_idx((goal_xy[2 * t] + P.pm.off_x + 0.5 * P.pm.unit) / P.pm.unit, W);
+  const int si = clamp_idx((y + P.pm.off_y + 0.5 * P.pm.unit) / P.pm.unit, H);
+  const int sj = clamp_idx((x + P.pm.off_x + 0.5 * P.pm.unit) / P.pm.unit, W);
+  const int gi = clamp_idx((gy + P.pm.off_y + 0.5 * P.pm.unit) / P.pm.unit, H);
+  const int gj = clamp_idx((gx + P.pm.off_x + 0.5 * P.pm.unit) / P.pm.unit, W);
   const int16_t* d = bfs + (int64_t)(gi * W + gj) * (H * W);
   int bi = si, bj = sj;
   const int di[4] = {-1, 0, 1, 0}, dj[4] = {0, -1, 0, 1};
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    int ni = si + di[k], nj = sj + dj[k];
-    if (ni >= 0 && ni < H && nj >= 0 && nj < W && wall_s[ni * W + nj] == 0 &&
-        d[ni * W + nj] < d[bi * W + bj]) {
+    const int ni = si + di[k], nj = sj + dj[k];
+    if (ni >= 0 && ni < H && nj >= 0 && nj < W && wall_s[ni * W + nj] == 0 && d[ni * W + nj] < d[bi * W + bj]) {
       bi = ni;
       bj = nj;
     }
   }
-  sub_xy[2 * t] = bj * P.pm.unit - P.pm.off_x;
-  sub_xy[2 * t + 1] = bi * P.pm.unit - P.pm.off_y;
+  *sx_out = bj * P.pm.unit - P.pm.off_x;
+  *sy_out = bi * P.pm.unit - P.pm.off_y;
+}
+
+__global__ void oracle_subgoal_kernel(const MazeParams* __restrict__ Pp, const int16_t* bfs, const double* start_xy,
+                                      const double* goal_xy, int64_t n, double* sub_xy) {
+  const MazeParams& P = *Pp;
+  __shared__ uint8_t wall_s[kMaxCells];
+  stage_wall(P, wall_s);
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  subgoal_of(P, wall_s, bfs, start_xy[2 * t], start_xy[2 * t + 1], goal_xy[2 * t], goal_xy[2 * t + 1],
+             &sub_xy[2 * t], &sub_xy[2 * t + 1]);
+}
+
+// Point-maze expert of data_gen_scripts/generate_locomaze.py:147-166 (the
+// point actor returns the subgoal direction, :44-46):
+//   dir = (subgoal - xy) / (||subgoal - xy|| + 1e-6),  ||v|| = sqrt(fma(vy, vy, vx*vx))
+//   (np.linalg.norm of a 1-D pair goes through BLAS ddot), action =
+//   clip(dir + normal, -1, 1) with normal = np.random.normal(0, noise, 2)
+//   (injected, or noise * Box-Muller(Philox)).  float64 actions.
+__global__ void expert_action_kernel(const MazeParams* __restrict__ Pp, const int16_t* bfs, const double* start_xy,
+                                     const double* goal_xy, int64_t n, double noise, const double* normal,
+                                     uint32_t k0, uint32_t k1, uint32_t call_lo, uint32_t call_hi,
+                                     double* action) {
+  const MazeParams& P = *Pp;
+  __shared__ uint8_t wall_s[kMaxCells];
+  stage_wall(P, wall_s);
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const double x = start_xy[2 * t], y = start_xy[2 * t + 1];
+  double sx, sy;
+  subgoal_of(P, wall_s, bfs, x, y, goal_xy[2 * t], goal_xy[2 * t + 1], &sx, &sy);
+  const double dx = sx - x, dy = sy - y;
+  const double den = sqrt(fma(dy, dy, dx * dx)) + 1e-6;
+  const double ux = dx / den, uy = dy / den;
+  double nx, ny;
+  if (normal != nullptr) {
+    nx = normal[2 * t];
+    ny = normal[2 * t + 1];
+  } else {
+    const u32x4 w = philox4x32_10({(uint32_t)t, call_lo, 0x45u, (uint32_t)(t >> 32) ^ call_hi}, k0, k1);
+    const double u1 = 1.0 - u01_from(w.x, w.y);  // (0, 1]
+    const double u2 = u01_from(w.z, w.w);
+    const double r = sqrt(-2.0 * log(u1));
+    const double a = 6.283185307179586 * u2;
+    nx = 0.0 + noise * (r * cos(a));
+    ny = 0.0 + noise * (r * sin(a));
+  }
+  double ax = ux + nx, ay = uy + ny;
+  ax = ax < -1.0 ? -1.0 : (ax > 1.0 ? 1.0 : ax);
+  ay = ay < -1.0 ? -1.0 : (ay > 1.0 ? 1.0 : ay);
+  action[2 * t] = ax;
+  action[2 * t + 1] = ay;
+}
+
+// MazeEnv.set_goal(goal_ij) (maze.py:492-501) for the envs with mask[i] != 0:
+// goal = ij_to_xy(goal_ij) (+ add_noise: uniform(-1,1)*unit/4 per axis,
+// injected or Philox).
+__global__ void set_goal_kernel(const MazeParams* __restrict__ Pp, MazeState S, int64_t n, const int32_t* goal_ij,
+                                const uint8_t* mask, const double* noise, uint32_t k0, uint32_t k1, uint32_t call_lo,
+                                uint32_t call_hi) {
+  const MazeParams& P = *Pp;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || (mask != nullptr && mask[i] == 0)) return;
+  double gx = goal_ij[2 * i + 1] * P.pm.unit - P.pm.off_x;
+  double gy = goal_ij[2 * i] * P.pm.unit - P.pm.off_y;
+  if (P.add_noise_to_goal) {
+    double r0, r1;
+    if (noise != nullptr) {
+      r0 = noise[2 * i];
+      r1 = noise[2 * i + 1];
+    } else {
+      const u32x4 w = philox4x32_10({(uint32_t)i, call_lo, 0x47u, (uint32_t)(i >> 32) ^ call_hi}, k0, k1);
+      r0 = -1.0 + 2.0 * u01_from(w.x, w.y);
+      r1 = -1.0 + 2.0 * u01_from(w.z, w.w);
+    }
+    gx = gx + r0 * P.pm.unit / 4.0;
+    gy = gy + r1 * P.pm.unit / 4.0;
+  }
+  reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
 }
 
 // ------------------------------------------------------------- host tables
@@ -805,6 +879,35 @@ ogbx_status ogbx_maze_oracle_subgoal(ogbx_maze_t e, const double* start_xy, cons
   hipLaunchKernelGGL(oracle_subgoal_kernel, dim3(grid_for(n, 256)), dim3(256), 0,
                      (hipStream_t)stream, e->Pd, e->bfs, start_xy, goal_xy, n, subgoal_xy);
   OGBX_LAUNCHED("oracle_subgoal_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_expert_action(ogbx_maze_t e, const double* start_xy, const double* goal_xy, int64_t n,
+                                   double noise, const double* normal, uint64_t seed, uint64_t call_index,
+                                   double* action, void* stream) {
+  OGBX_CHECK(e != nullptr && action, OGBX_EINVAL, "ogbx_maze_expert_action: null argument");
+  OGBX_CHECK((start_xy && goal_xy) || n == e->n, OGBX_EINVAL,
+             "ogbx_maze_expert_action: n must equal the batch size when reading the env state");
+  if (n <= 0) return OGBX_OK;
+  OGBX_HIP(hipSetDevice(e->device));
+  uint32_t k0, k1;
+  seed_key(seed, kTagMazeExpert, &k0, &k1);
+  hipLaunchKernelGGL(expert_action_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, e->Pd,
+                     e->bfs, start_xy ? start_xy : e->S.qpos, goal_xy ? goal_xy : e->S.goal, n, noise, normal, k0,
+                     k1, (uint32_t)call_index, (uint32_t)(call_index >> 32), action);
+  OGBX_LAUNCHED("expert_action_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_set_goal(ogbx_maze_t e, const int32_t* goal_ij, const uint8_t* mask, const double* noise,
+                               uint64_t seed, uint64_t call_index, void* stream) {
+  OGBX_CHECK(e != nullptr && goal_ij, OGBX_EINVAL, "ogbx_maze_set_goal: null argument");
+  OGBX_HIP(hipSetDevice(e->device));
+  uint32_t k0, k1;
+  seed_key(seed, kTagMazeGoal, &k0, &k1);
+  hipLaunchKernelGGL(set_goal_kernel, dim3(grid_for(e->n, 256)), dim3(256), 0, (hipStream_t)stream, e->Pd, e->S,
+                     e->n, goal_ij, mask, noise, k0, k1, (uint32_t)call_index, (uint32_t)(call_index >> 32));
+  OGBX_LAUNCHED("set_goal_kernel");
   return OGBX_OK;
 }
 

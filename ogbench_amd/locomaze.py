@@ -228,6 +228,43 @@ class MazeEnv:
         )
         return out
 
+    def expert_action(self, noise=0.2, normal=None, start_xy=None, goal_xy=None, out=None, seed=None):
+        """Point-maze expert of data_gen_scripts/generate_locomaze.py:147-166:
+        clip(subgoal direction + N(0, noise), -1, 1) as float64 [N,2] (one launch).
+
+        Without start_xy/goal_xy it reads the envs' own qpos and goal (no host
+        round trip).  normal: injected np.random.normal(0, noise) draws [N,2]."""
+        torch = _torch()
+        n = self.num_envs if start_xy is None else int(start_xy.shape[0])
+        if out is None:
+            out = torch.empty(n, 2, dtype=torch.float64, device=self.device)
+        s = g = None
+        if start_xy is not None or goal_xy is not None:
+            assert start_xy is not None and goal_xy is not None, 'give both start_xy and goal_xy'
+            s = start_xy.to(self.device, torch.float64).contiguous()
+            g = goal_xy.to(self.device, torch.float64).contiguous()
+        z = None if normal is None else torch.as_tensor(normal).to(self.device, torch.float64).contiguous()
+        calls = getattr(self, '_expert_calls', 0)
+        self._expert_calls = calls + 1
+        sd = seed if seed is not None else (self._seed if self._seed is not None else 0)
+        _lib.check(self._L.ogbx_maze_expert_action(self._h, _lib.ptr(s), _lib.ptr(g), n, float(noise), _lib.ptr(z),
+                                                    int(sd) & ((1 << 64) - 1), calls, _lib.ptr(out),
+                                                    self._stream()), 'expert_action')
+        return out
+
+    def set_goal(self, goal_ij, mask=None, noise=None):
+        """MazeEnv.set_goal(goal_ij) (maze.py:492-501) per env: goal_ij int [N,2]
+        (+ add_noise draws from Philox, or injected uniform(-1,1) `noise` [N,2])."""
+        torch = _torch()
+        ij = torch.as_tensor(goal_ij).to(self.device, torch.int32).reshape(self.num_envs, 2).contiguous()
+        m = None if mask is None else torch.as_tensor(mask).to(self.device, torch.uint8).contiguous()
+        z = None if noise is None else torch.as_tensor(noise).to(self.device, torch.float64).contiguous()
+        calls = getattr(self, '_goal_calls', 0)
+        self._goal_calls = calls + 1
+        sd = self._seed if self._seed is not None else 0
+        _lib.check(self._L.ogbx_maze_set_goal(self._h, _lib.ptr(ij), _lib.ptr(m), _lib.ptr(z), int(sd), calls,
+                                              self._stream()), 'set_goal')
+
     def _state_ptrs(self):
         q, g, e, t, ep = (_lib.c_void_p() for _ in range(5))
         _lib.check(self._L.ogbx_maze_state(self._h, q, g, e, t, ep))

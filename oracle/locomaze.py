@@ -65,6 +65,16 @@ def oracle_subgoal(maze, start_xy, goal_xy):
     return out
 
 
+def expert_action(maze, xy, goal_xy, normal):
+    """generate_locomaze.py point expert with injected normal draws [n,2]."""
+    xy = np.ascontiguousarray(xy, np.float64)
+    g = np.ascontiguousarray(goal_xy, np.float64)
+    z = np.ascontiguousarray(normal, np.float64)
+    out = np.zeros_like(xy)
+    lib().orc_expert_action(maze.encode(), _p(xy), _p(g), _p(z), ctypes.c_int64(len(xy)), _p(out))
+    return out
+
+
 def _opts(success_pre=0, terminate_at_goal=1, add_noise_to_goal=1, reward_task_id=-1, max_steps=1000,
           not_point=0):
     return np.array([success_pre, terminate_at_goal, add_noise_to_goal, reward_task_id, max_steps, not_point],

@@ -525,3 +525,25 @@ int orc_oracle_subgoal(const char* maze, const double* start_xy, const double* g
   free(qu);
   return 0;
 }
+
+/* Point-maze expert action (data_gen_scripts/generate_locomaze.py:147-166, the
+ * point actor :44-46) with injected np.random.normal draws `normal` [n,2]:
+ * dir = d / (sqrt(fma(dy, dy, dx*dx)) + 1e-6) (np.linalg.norm of a 1-D pair via
+ * BLAS ddot), action = clip(dir + normal, -1, 1). */
+int orc_expert_action(const char* maze, const double* xy, const double* goal_xy, const double* normal, int64_t n,
+                      double* action) {
+  double* sub = (double*)malloc(sizeof(double) * 2 * (n > 0 ? n : 1));
+  if (orc_oracle_subgoal(maze, xy, goal_xy, n, sub) != 0) {
+    free(sub);
+    return -1;
+  }
+  for (int64_t t = 0; t < n; ++t) {
+    const double dx = sub[2 * t] - xy[2 * t], dy = sub[2 * t + 1] - xy[2 * t + 1];
+    const double den = sqrt(fma(dy, dy, dx * dx)) + 1e-6;
+    double a0 = dx / den + normal[2 * t], a1 = dy / den + normal[2 * t + 1];
+    action[2 * t] = a0 < -1.0 ? -1.0 : (a0 > 1.0 ? 1.0 : a0);
+    action[2 * t + 1] = a1 < -1.0 ? -1.0 : (a1 > 1.0 ? 1.0 : a1);
+  }
+  free(sub);
+  return 0;
+}
