@@ -448,6 +448,26 @@ int orc_maze_step(const char* maze, const int* opts_i, double* qpos, double* goa
       y = y + dy;
       point_step(mz, &C, &x, &y);
       if (!o.success_pre) s = success_of(x, y, gx, gy, o.goal_tol);
+      const double ox = x, oy = y; /* ob is taken before a teleport (maze.py:437-451) */
+      if (strcmp(maze, "teleport") == 0) {
+        /* teleport maze portals (maze.py:149-161): in (4,6), (5,1); out (1,7),
+         * (6,1), (6,10); radius 1, triggered within 1.5 (norm as success_of).
+         * The out portal is the libogbx Philox draw (key (k0 ^ 0x4D5A0002, k1),
+         * counter (i, episode, 0x100 + elapsed, hi32(i))), in place of
+         * np.random.randint(3). */
+        static const int tin[2][2] = {{4, 6}, {5, 1}}, tout[3][2] = {{1, 7}, {6, 1}, {6, 10}};
+        for (int t = 0; t < 2; ++t) {
+          double px, py;
+          ij_to_xy(tin[t][0], tin[t][1], &px, &py);
+          if (success_of(x, y, px, py, 1.0 * 1.5)) {
+            uint32_t c[4] = {(uint32_t)i, ep, 0x100u + (uint32_t)el, (uint32_t)((uint64_t)i >> 32)};
+            philox(c, k0 ^ 0x4D5A0002u, k1);
+            const int oidx = (int)(((uint64_t)c[0] * 3u) >> 32);
+            ij_to_xy(tout[oidx][0], tout[oidx][1], &x, &y);
+            break;
+          }
+        }
+      }
       float rw = s ? 1.0f : 0.0f;
       if (o.reward_task_id > 0) rw -= 1.0f;
       int te = s && o.terminate_at_goal;
@@ -464,8 +484,13 @@ int orc_maze_step(const char* maze, const int* opts_i, double* qpos, double* goa
         reset_env(mz, &o, task[i], r, &x, &y, &gx, &gy);
         el = 0;
       }
-      obs[2 * oi] = x;
-      obs[2 * oi + 1] = y;
+      double wx = ox, wy = oy;
+      if (auto_reset && (te || tr)) {
+        wx = x;
+        wy = y;
+      }
+      obs[2 * oi] = wx;
+      obs[2 * oi + 1] = wy;
     }
     qpos[2 * i] = x;
     qpos[2 * i + 1] = y;

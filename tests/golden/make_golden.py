@@ -175,6 +175,18 @@ def locomaze_golden(rng):
     return out
 
 
+def teleport_golden():
+    """The teleport maze portal table (maze.py:149-161), read from the source."""
+    src = _maze_source()
+    m = re.search(r"self\._teleport_info = dict\((.*?)\n\s*\)", src, re.S)
+    body = m.group(1)
+    info = {}
+    for key in ('teleport_in_ijs', 'teleport_out_ijs', 'teleport_radius'):
+        v = re.search(key + r"=(\[.*?\]|[0-9.]+)", body, re.S).group(1)
+        info[key] = ast.literal_eval(v)
+    return info
+
+
 def registry_golden():
     """max_episode_steps / kwargs of every locomaze + powderworld id."""
     src = open(os.path.join(REF, 'ogbench/locomaze/__init__.py')).read()
@@ -206,6 +218,8 @@ def main():
     with open(os.path.join(OUT, 'registry_golden.json'), 'w') as f:
         json.dump(reg, f, indent=0, sort_keys=True)
     print('wrote', sorted(lm.keys())[:5], '...', len(reg), 'registry entries')
+    with open(os.path.join(OUT, 'teleport_golden.json'), 'w') as f:
+        json.dump(teleport_golden(), f, indent=0, sort_keys=True)
     for extra in ('make_golden_powder', 'make_golden_gc'):
         path = os.path.join(OUT, extra + '.py')
         if os.path.exists(path):

@@ -158,3 +158,33 @@ def test_teleport_moves_state_but_not_obs(gpu):
     assert np.array_equal(obs.cpu().numpy()[0], [20.0, 12.0])
     assert tuple(q[0]) in {(24.0, 0.0), (0.0, 20.0), (36.0, 20.0)}
     assert np.array_equal(q[1], [5.0, 0.0])
+
+
+def test_teleport_maze_matches_oracle(gpu):
+    """Teleport maze: agents around the in-portals, 3 fused steps; the GPU and
+    the oracle (same Philox key for the out-portal draw) agree on every
+    teleport destination bit-exactly and on the dynamics to TOL."""
+    rng = np.random.RandomState(21)
+    n = 20000
+    ins = np.array([[20.0, 12.0], [0.0, 16.0]])
+    centre = ins[np.arange(n) % 2]
+    ang = rng.uniform(0, 2 * np.pi, n)
+    q = centre + np.stack([np.cos(ang), np.sin(ang)], 1) * rng.uniform(0, 2.2, n)[:, None]
+    env = _env(gpu, n, 'teleport')
+    env.reset(seed=77, options=dict(task_id=1))
+    sd = env.state_dict()
+    sd['qpos'] = torch.tensor(q, device=gpu)
+    env.load_state_dict(sd)
+    st = dict(qpos=q.copy(), goal=sd['goal'].cpu().numpy().copy(), elapsed=sd['elapsed'].cpu().numpy().copy(),
+              task=sd['task'].cpu().numpy().copy(), episode=sd['episode'].cpu().numpy().view(np.uint32).copy(),
+              opts=orc._opts())
+    a = rng.uniform(-1, 1, (3, n, 2)).astype(np.float32)
+    out = env.rollout(torch.tensor(a, device=gpu))
+    ref = orc.step('teleport', st, a, key=orc.philox_key(77, orc.TAG_MAZE_RESET))
+    got_q = env.get_xy().cpu().numpy()
+    assert np.abs(out['obs'].cpu().numpy() - ref['obs']).max() <= TOL
+    assert np.abs(got_q - st['qpos']).max() <= TOL
+    outs = np.array([[24.0, 0.0], [0.0, 20.0], [36.0, 20.0]])
+    tele = (np.abs(st['qpos'][:, None, :] - outs[None]).max(-1) == 0).any(1)
+    assert tele.sum() > 200  # teleported at the last step (earlier ones moved on; all are checked above)
+    assert np.array_equal(got_q[tele], st['qpos'][tele])
