@@ -147,16 +147,49 @@ struct Blk {
 
   __device__ __forceinline__ const uint8_t* row(const uint8_t* base, int R) const { return base + R * G::W + c0; }
 
+  // ---- SWAR helpers: four cells per 32-bit word (byte k = cell 4j+k)
+  static constexpr uint32_t kLo7 = 0x7F7F7F7Fu, kHi = 0x80808080u, kOnes = 0x01010101u;
+  static constexpr uint32_t kIds = 0x1F1F1F1Fu, kGravB = 0x20202020u, kDidgB = 0x40404040u;
+  // 0x80 in every byte that is zero, else 0 (exact per byte: no carries)
+  __device__ static __forceinline__ uint32_t zbytes(uint32_t y) { return ~(((y & kLo7) + kLo7) | y | kLo7); }
+  // 0x80 flags -> 0xFF byte masks
+  __device__ static __forceinline__ uint32_t bmask(uint32_t f) { return (f >> 7) * 0xFFu; }
+  // bytes 3..6 of {hi:lo} (hi << 8 | lo >> 24): the left neighbours of hi's cells
+  __device__ static __forceinline__ uint32_t left_of(uint32_t hi, uint32_t lo) {
+    return __builtin_amdgcn_alignbyte(hi, lo, 3);
+  }
+  // bytes 1..4 of {hi:lo}: the right neighbours of lo's cells
+  __device__ static __forceinline__ uint32_t right_of(uint32_t hi, uint32_t lo) {
+    return __builtin_amdgcn_alignbyte(hi, lo, 1);
+  }
+  // density (channel 1) of every byte's element id, v_perm_b32 byte tables
+  __device__ static __forceinline__ uint32_t dens4(uint32_t w) {
+    constexpr uint32_t d0 = pack4(0), d1 = pack4(4), d2 = pack4(8), d3 = pack4(12), d4 = pack4(16), d5 = pack4(20);
+    const uint32_t id = w & kIds, sel = id & 0x07070707u;
+    const uint32_t t0 = __builtin_amdgcn_perm(d1, d0, sel);
+    const uint32_t t1 = __builtin_amdgcn_perm(d3, d2, sel);
+    const uint32_t t2 = __builtin_amdgcn_perm(d5, d4, sel);
+    const uint32_t b3 = ((id >> 3) & kOnes) * 0xFFu, b4 = ((id >> 4) & kOnes) * 0xFFu;
+    return (t2 & b4) | (~b4 & ((t1 & b3) | (t0 & ~b3)));
+  }
+  static constexpr uint32_t pack4(int i) {
+    uint32_t v = 0;
+    for (int k = 0; k < 4; ++k) v |= (uint32_t)(i + k < 21 ? kDensity[i + k] : 0) << (8 * k);
+    return v;
+  }
+
   // BehaviorStone (sim.py:580-590) for one row segment: a stone keeps gravity
   // unless both up-left and up-right neighbours are stone (zero-padded conv).
+  // upL / upR: the up row's bytes just left / right of the segment (0 outside).
   __device__ __forceinline__ S stone(S cur, const S& up, uint32_t upL, uint32_t upR, bool has_up) const {
 #pragma unroll
-    for (int k = 0; k < G::CPT; ++k) {
-      const uint32_t v = cur.get(k);
-      const uint32_t ul = k == 0 ? upL : up.get(k - 1);
-      const uint32_t ur = k == G::CPT - 1 ? upR : up.get(k + 1);
-      const bool both = has_up && (ul & kIdMask) == 9u && (ur & kIdMask) == 9u;
-      if ((v & kIdMask) == 9u) cur.set(k, (v & ~kGrav) | (both ? 0u : kGrav));
+    for (int j = 0; j < G::NW; ++j) {
+      const uint32_t ul = left_of(up.w[j], j == 0 ? (upL << 24) : up.w[j - 1]);
+      const uint32_t ur = right_of(j == G::NW - 1 ? upR : up.w[j + 1], up.w[j]);
+      const uint32_t st = zbytes((cur.w[j] & kIds) ^ 0x09090909u);
+      uint32_t both = zbytes((ul & kIds) ^ 0x09090909u) & zbytes((ur & kIds) ^ 0x09090909u);
+      both = has_up ? both : 0u;
+      cur.w[j] = (cur.w[j] & ~(st >> 2)) | ((st & ~both) >> 2);
     }
     return cur;
   }
@@ -167,6 +200,8 @@ struct Blk {
   __device__ __forceinline__ uint32_t right_byte(const uint8_t* base, int R) const {
     return c0 + G::CPT < G::W ? base[R * G::W + c0 + G::CPT] : 0u;
   }
+  // BehaviorGravity's did-gravity reset: clear bit 6 where bit 5 (gravity) is set
+  __device__ static __forceinline__ uint32_t rd4(uint32_t x) { return x & ~((x & kGravB) << 1); }
 
   // One PWSim.forward (stone rule, then gravity with periodic rolls) followed
   // by the brush paint (powderworld_env.py:380-391), own = this thread's
@@ -183,32 +218,38 @@ struct Blk {
     const S b_0 = stone(own, a_m1, left_byte(A, rm1), right_byte(A, rm1), r > 0);
     const S b_p1 = stone(a_p1, own, left_byte(A, r), right_byte(A, r), rp1 > 0);
     // BehaviorGravity (sim.py:476-501): a cell moves down when the cell below
-    // is lighter and both have gravity
+    // is lighter and both have gravity (0x80 flags per byte)
     S dbb;
 #pragma unroll
-    for (int k = 0; k < G::NW; ++k) dbb.w[k] = 0;
-#pragma unroll
-    for (int k = 0; k < G::CPT; ++k) {
-      const uint32_t v = b_0.get(k), w = b_p1.get(k);
-      const bool m = dens_of(w) < dens_of(v) && (v & kGrav) && (w & kGrav);
-      if (m) dbb.w[k >> 2] |= 1u << ((k & 3) * 8);
+    for (int j = 0; j < G::NW; ++j) {
+      const uint32_t dv = dens4(b_0.w[j]), dw = dens4(b_p1.w[j]);
+      const uint32_t lt = ((dv | kHi) - dw - kOnes) & kHi;  // dw < dv (values <= 7: no borrow)
+      const uint32_t g = (b_0.w[j] & b_p1.w[j] & kGravB) << 2;
+      dbb.w[j] = lt & g;
     }
     store_seg(sh.f + r * G::W + c0, dbb);
     __syncthreads();
     const S f_m1 = load_seg<G::NW>(row(sh.f, rm1));
     const S f_m2 = load_seg<G::NW>(row(sh.f, rm2));
     const bool in_rows = paint_id >= 0 && r >= ry && r < ry + brush;
-    const uint32_t pcell = paint_id >= 0 ? elem_cell((uint32_t)paint_id) : 0u;
+    const uint32_t pcell = paint_id >= 0 ? elem_cell((uint32_t)paint_id) * kOnes : 0u;
 #pragma unroll
-    for (int k = 0; k < G::CPT; ++k) {
-      // overlap resolution (sim.py:487-489): a cell that sinks onto a sinking
-      // cell stays; real moves are dbb & ~dbb(above)
-      const bool real0 = dbb.get(k) && !f_m1.get(k);
-      const bool realm1 = f_m1.get(k) && !f_m2.get(k);
-      uint32_t v = real0 ? rd(b_p1.get(k)) : (realm1 ? (rd(b_m1.get(k)) | kDidg) : rd(b_0.get(k)));
-      const int c = c0 + k;
-      if (in_rows && c >= rx && c < rx + brush && (v & kIdMask) != 1u) v = pcell;
-      own.set(k, v);
+    for (int j = 0; j < G::NW; ++j) {
+      // overlap resolution (sim.py:487-489): real moves are dbb & ~dbb(above)
+      const uint32_t m0 = bmask(dbb.w[j] & ~f_m1.w[j]);
+      const uint32_t m1 = bmask(f_m1.w[j] & ~f_m2.w[j]);
+      uint32_t v = (rd4(b_p1.w[j]) & m0) | (~m0 & (((rd4(b_m1.w[j]) | kDidgB) & m1) | (rd4(b_0.w[j]) & ~m1)));
+      if (in_rows) {
+        uint32_t pm = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int c = c0 + 4 * j + b;
+          pm |= (c >= rx && c < rx + brush) ? (0xFFu << (8 * b)) : 0u;
+        }
+        pm &= ~bmask(zbytes((v & kIds) ^ kOnes));  // not onto walls (id 1)
+        v = (pcell & pm) | (v & ~pm);
+      }
+      own.w[j] = v;
     }
     store_seg(sh.a + r * G::W + c0, own);
     __syncthreads();
@@ -224,17 +265,18 @@ struct Blk {
     const S up = load_seg<G::NW>(row(A, rm1));
     const S dn = load_seg<G::NW>(row(A, rp1));
     const S g = load_seg<G::NW>(goal + r * W + c0);
-    const uint32_t lft = A[r * W + (c0 == 0 ? W - 1 : c0 - 1)];
-    const uint32_t rgt = A[r * W + (c0 + G::CPT == W ? 0 : c0 + G::CPT)];
+    const uint32_t lft = A[r * W + (c0 == 0 ? W - 1 : c0 - 1)] & kIdMask;
+    const uint32_t rgt = A[r * W + (c0 + G::CPT == W ? 0 : c0 + G::CPT)] & kIdMask;
     int err = 0;
 #pragma unroll
-    for (int k = 0; k < G::CPT; ++k) {
-      const uint32_t gk = g.get(k);
-      const uint32_t l = k == 0 ? lft : own.get(k - 1);
-      const uint32_t rr = k == G::CPT - 1 ? rgt : own.get(k + 1);
-      const bool m = (own.get(k) & kIdMask) == gk || (l & kIdMask) == gk || (rr & kIdMask) == gk ||
-                     (up.get(k) & kIdMask) == gk || (dn.get(k) & kIdMask) == gk;
-      err += m ? 0 : 1;
+    for (int j = 0; j < G::NW; ++j) {
+      const uint32_t o = own.w[j] & kIds;
+      const uint32_t lo = j == 0 ? (lft << 24) : (own.w[j - 1] & kIds);
+      const uint32_t hi = j == G::NW - 1 ? rgt : (own.w[j + 1] & kIds);
+      const uint32_t gk = g.w[j];
+      const uint32_t m = zbytes(gk ^ o) | zbytes(gk ^ left_of(o, lo)) | zbytes(gk ^ right_of(hi, o)) |
+                         zbytes(gk ^ (up.w[j] & kIds)) | zbytes(gk ^ (dn.w[j] & kIds));
+      err += __builtin_popcount(~m & kHi);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
