@@ -80,23 +80,24 @@ def _timed(fn, steps, world, dev):
 
 
 def _per_launch_ms(fn, launches, dev, host_us=120.0):
-    """Average device duration of single launches: HIP event pair around each
-    launch, on the stream the kernel runs on (torch's current stream).
+    """Average device duration of one launch: `launches` launches queued back
+    to back between one HIP event pair on the stream the kernel runs on
+    (torch's current stream), divided by the count.
 
     A spin kernel (torch.cuda._sleep) is queued first, long enough for the host
-    to enqueue every event pair and launch behind it; the pairs then time the
-    kernels back to back instead of the host's launch gaps (a host-bound call
+    to enqueue every launch behind it, so the span covers the kernels (and the
+    dispatch gaps between them), not the host's launch rate (a host-bound call
     such as GCDataset.sample(1024) would otherwise read as its host time)."""
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     torch.cuda._sleep(int(launches * host_us * 1e-6 * 2.4e9))
-    for i, (a, b) in enumerate(ev):
-        a.record(stream)
+    a.record(stream)
+    for i in range(launches):
         fn(i)
-        b.record(stream)
+    b.record(stream)
     torch.cuda.synchronize(dev)
-    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return a.elapsed_time(b) / launches
 
 
 def _traffic(kernel, kern_ms):

@@ -14,7 +14,7 @@ ROUND=${ROUND:-r01}
 STEPS=${STEPS:-300}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-ARGS="--workload $WL --steps $STEPS --warmup 20 --no-cpu-baseline --no-extras"
+ARGS="--workload $WL --steps $STEPS --warmup ${WARMUP:-100} --no-cpu-baseline --no-extras"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$WL -o run --output-format csv -- \
   python3 bench.py $ARGS > gpurun_out/prof_${WL}.log 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$WL -o run --output-format csv -- \
