@@ -503,61 +503,6 @@ static const MazeSpec kMazes[] = {
      5, {{1, 10, 7, 1}, {1, 1, 7, 10}, {5, 6, 7, 10}, {7, 1, 7, 10}, {5, 6, 7, 1}}},
 };
 
-// MuJoCo-derived constants of the point model (DESIGN.md lists each source).
-static PointModel make_point_model(double unit, double off) {
-  PointModel pm{};
-  const double pi = 3.14159265358979323846;
-  const double r = 0.7, density = 100.0;
-  pm.mass = density * (4.0 * pi * r * r * r / 3.0);
-  pm.h = 0.02;
-  pm.nsub = 5;
-  // solref (0.02, 1) with refsafe: timeconst = max(0.02, 2*dt) = 0.04
-  const double timeconst = std::fmax(0.02, 2.0 * pm.h), dampratio = 1.0;
-  // solimp (0.9, 0.95, 0.001, 0.5, 2)
-  pm.imp_dmin = 0.9;
-  pm.imp_dmax = 0.95;
-  pm.imp_width = 0.001;
-  pm.imp_mid = 0.5;
-  const double power = 2.0;
-  pm.imp_a = 1.0 / std::pow(pm.imp_mid, power - 1.0);
-  pm.imp_b = 1.0 / std::pow(1.0 - pm.imp_mid, power - 1.0);
-  const double dmax = pm.imp_dmax;
-  pm.K = 1.0 / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
-  pm.B = 2.0 / (dmax * timeconst);
-  // body_invweight0 (translation) = mean diag of J M^-1 J' over 3 axes = 2/(3m);
-  // pyramid edge diagApprox = tran + mu^2 * tran with mu = 1.
-  const double tran = (1.0 / pm.mass + 1.0 / pm.mass + 0.0) / 3.0;
-  const double mu = 1.0;
-  pm.diag = tran + mu * mu * tran;
-  double Rf = (1.0 - pm.imp_dmin) * pm.diag / pm.imp_dmin;
-  if (Rf < kMinVal) Rf = kMinVal;
-  // Floor: four edges +-e_x, +-e_y, each with D = 1/Rf; exactly one edge of
-  // each pair is active, which sums to 1/2 Df |a + B v|^2.
-  pm.D_floor = 1.0 / Rf;
-  pm.radius = r;
-  pm.r2_hi = r * r * (1.0 + 1e-12);
-  pm.sphere_z = 0.7;
-  pm.box_cz = 0.5 / 2.0 * unit;  // maze_height/2 * maze_unit (maze.py:233)
-  pm.box_hz = 0.5 / 2.0 * unit;
-  pm.box_hxy = unit / 2.0;
-  pm.unit = unit;
-  pm.inv_unit = 1.0 / unit;  // exact for unit = 4
-  pm.off_x = off;
-  pm.off_y = off;
-  // solver constants
-  pm.M = pm.mass + pm.D_floor;
-  pm.m_over_M = pm.mass / pm.M;
-  double Rmax = (1.0 - dmax) * pm.diag / dmax;
-  if (Rmax < kMinVal) Rmax = kMinVal;
-  pm.w_max = 1.0 / Rmax;
-  pm.kp_max = pm.K * dmax;
-  const double w = pm.w_max, M = pm.M;
-  pm.inv_M2w = 1.0 / (M + 2.0 * w);
-  pm.inv_M4w = 1.0 / (M + 4.0 * w);
-  pm.inv_det3 = 1.0 / ((M + 3.0 * w) * (M + w) - w * w);
-  pm.inv_width = 1.0 / pm.imp_width;
-  return pm;
-}
 
 static void build_bfs(const MazeParams& P, std::vector<int16_t>& out) {
   const int H = P.H, W = P.W, C = H * W;
