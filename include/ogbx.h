@@ -208,6 +208,10 @@ typedef struct {
   int64_t num_valid;         /* (NULL -> randint(R), datasets.py:65-70)          */
   const int64_t* traj_end;   /* device [R]: terminal_locs[searchsorted(
                                 terminal_locs, row)] (datasets.py:309)           */
+  const int64_t* valid_traj_end; /* optional device [num_valid] =
+                                traj_end[valid_idxs]: lets a drawn index and its
+                                trajectory end load in parallel (NULL = two
+                                dependent loads)                                  */
 } ogbx_gc_buffer;
 
 /* Goal-sampling configuration (GCDataset config keys, datasets.py:155-170).

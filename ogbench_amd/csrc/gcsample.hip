@@ -14,7 +14,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -84,11 +86,72 @@ __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, 
   }
 }
 
+// Copy every column row of a tile.  For small tiles (latency-bound launches)
+// whose columns are all 4-byte granular (float32 data), the (column, sample,
+// word) items of the whole tile form one
+// flat index space and each thread issues kUnroll loads before its stores, so
+// the columns' HBM round trips overlap instead of running one after another.
+// Otherwise each column is copied with its widest aligned unit.
+template <int kSel>
+__device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int64_t (*sel)[kGcMaxTile], int64_t base,
+                                 int n_here, bool flat4) {
+  if (flat4) {
+    constexpr int kUnroll = 4;
+    __shared__ int s_pre[kGcMaxCols + 1];
+    if (threadIdx.x == 0) {
+      int acc = 0;
+      for (int c = 0; c < num_cols; ++c) {
+        s_pre[c] = acc;
+        acc += (int)(cols.c[c].row_bytes >> 2) * n_here;
+      }
+      s_pre[num_cols] = acc;
+    }
+    __syncthreads();
+    const int total = s_pre[num_cols];
+    for (int f0 = threadIdx.x; f0 < total; f0 += blockDim.x * kUnroll) {
+      uint32_t v[kUnroll];
+      uint32_t* d[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int f = f0 + u * (int)blockDim.x;
+        d[u] = nullptr;
+        if (f < total) {
+          int c = 0;
+          while (s_pre[c + 1] <= f) ++c;
+          const ogbx_gc_column& col = cols.c[c];
+          const int units = (int)(col.row_bytes >> 2);
+          const int rel = f - s_pre[c];
+          const int b = rel / units, k = rel - b * units;
+          v[u] = ((const uint32_t*)col.src)[sel[col.select][b] * units + k];
+          d[u] = (uint32_t*)col.dst + (base + b) * units + k;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+        if (d[u]) *d[u] = v[u];
+    }
+    return;
+  }
+  for (int c = 0; c < num_cols; ++c) {
+    const ogbx_gc_column& col = cols.c[c];
+    const int64_t* srow = sel[col.select];
+    const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst;
+    if (col.row_bytes % 16 == 0 && align % 16 == 0)
+      copy_rows<uint4>(col, srow, base, n_here);
+    else if (col.row_bytes % 8 == 0 && align % 8 == 0)
+      copy_rows<uint2>(col, srow, base, n_here);
+    else if (col.row_bytes % 4 == 0 && align % 4 == 0)
+      copy_rows<uint32_t>(col, srow, base, n_here);
+    else
+      copy_rows<uint8_t>(col, srow, base, n_here);
+  }
+}
+
 __global__ void __launch_bounds__(256) gc_sample_kernel(
     ogbx_gc_buffer buf, ogbx_gc_config cfg, GcColumns cols, int32_t num_cols, int64_t total,
     int tile, ogbx_gc_draws dr, uint32_t k0, uint32_t k1, uint32_t call_lo, uint32_t call_hi,
     double v_log_q, double a_log_q, int64_t* idxs_out, int64_t* vgoal_out, int64_t* agoal_out,
-    double* masks, double* rewards, ogbx_gc_draw_record rec) {
+    double* masks, double* rewards, ogbx_gc_draw_record rec, bool flat4) {
   __shared__ int64_t sel[4][kGcMaxTile];
   const int64_t base = (int64_t)blockIdx.x * tile;
   int n_here = (int)((total - base) < tile ? (total - base) : tile);
@@ -110,7 +173,7 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
       pick = dr.pick ? dr.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
       idx = buf.valid_idxs ? buf.valid_idxs[pick] : pick;
     }
-    const int64_t final_idx = buf.traj_end[idx];
+    const int64_t final_idx = (pick >= 0 && buf.valid_traj_end) ? buf.valid_traj_end[pick] : buf.traj_end[idx];
     const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
     GoalDraws v, a;
     v.pick = dr.v_pick ? dr.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
@@ -155,19 +218,7 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
     }
   }
   __syncthreads();
-  for (int c = 0; c < num_cols; ++c) {
-    const ogbx_gc_column& col = cols.c[c];
-    const int64_t* srow = sel[col.select];
-    const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst;
-    if (col.row_bytes % 16 == 0 && align % 16 == 0)
-      copy_rows<uint4>(col, srow, base, n_here);
-    else if (col.row_bytes % 8 == 0 && align % 8 == 0)
-      copy_rows<uint2>(col, srow, base, n_here);
-    else if (col.row_bytes % 4 == 0 && align % 4 == 0)
-      copy_rows<uint32_t>(col, srow, base, n_here);
-    else
-      copy_rows<uint8_t>(col, srow, base, n_here);
-  }
+  copy_tile<0>(cols, num_cols, sel, base, n_here, flat4);
 }
 
 // HGCDataset.compute_high_next_idxs (datasets.py:478-491) for one sample.
@@ -188,7 +239,7 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, GcColumns cols, int32_t num_cols,
     int64_t total, int tile, ogbx_hgc_draws dr, uint32_t k0, uint32_t k1, uint32_t call_lo,
     uint32_t call_hi, double v_log_q, double a_log_q, double l_log_q, ogbx_hgc_outputs o,
-    ogbx_hgc_draw_record rec) {
+    ogbx_hgc_draw_record rec, bool flat4) {
   __shared__ int64_t sel[kHgcSel][kGcMaxTile];
   const int64_t base = (int64_t)blockIdx.x * tile;
   const int n_here = (int)((total - base) < tile ? (total - base) : tile);
@@ -210,7 +261,7 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
       pick = g.pick ? g.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
       idx = buf.valid_idxs ? buf.valid_idxs[pick] : pick;
     }
-    const int64_t fin = buf.traj_end[idx];
+    const int64_t fin = (pick >= 0 && buf.valid_traj_end) ? buf.valid_traj_end[pick] : buf.traj_end[idx];
     const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
     GoalDraws v, a, l;
     v.pick = g.v_pick ? g.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
@@ -299,19 +350,7 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     }
   }
   __syncthreads();
-  for (int c = 0; c < num_cols; ++c) {
-    const ogbx_gc_column& col = cols.c[c];
-    const int64_t* srow = sel[col.select];
-    const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst;
-    if (col.row_bytes % 16 == 0 && align % 16 == 0)
-      copy_rows<uint4>(col, srow, base, n_here);
-    else if (col.row_bytes % 8 == 0 && align % 8 == 0)
-      copy_rows<uint2>(col, srow, base, n_here);
-    else if (col.row_bytes % 4 == 0 && align % 4 == 0)
-      copy_rows<uint32_t>(col, srow, base, n_here);
-    else
-      copy_rows<uint8_t>(col, srow, base, n_here);
-  }
+  copy_tile<0>(cols, num_cols, sel, base, n_here, flat4);
 }
 
 __global__ void traj_end_kernel(const int64_t* __restrict__ term, int64_t nterm, int64_t nrows,
@@ -336,6 +375,18 @@ struct PositiveF32 {
 }  // namespace ogbx
 
 using namespace ogbx;
+
+// Every column 4-byte granular and aligned, and the tile's word count small
+// enough for the flat int indexing of copy_tile.
+static bool flat4_columns(const GcColumns& cc, int num_cols) {
+  int64_t words = 0;
+  for (int i = 0; i < num_cols; ++i) {
+    const ogbx_gc_column& c = cc.c[i];
+    if (c.row_bytes % 4 != 0 || ((uintptr_t)c.src | (uintptr_t)c.dst) % 4 != 0) return false;
+    words += (c.row_bytes >> 2) * kGcMaxTile;
+  }
+  return words < (1ll << 30);
+}
 
 extern "C" {
 
@@ -376,7 +427,8 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
   hipLaunchKernelGGL(gc_sample_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
                      *buf, *cfg, cc, num_cols, total, (int)tile, dr, k0, k1,
                      (uint32_t)call_index, (uint32_t)(call_index >> 32), v_log_q, a_log_q,
-                     idxs_out, value_goal_out, actor_goal_out, masks, rewards, rec);
+                     idxs_out, value_goal_out, actor_goal_out, masks, rewards, rec,
+                     tile <= 4 && flat4_columns(cc, num_cols));
   OGBX_LAUNCHED("gc_sample_kernel");
   return OGBX_OK;
 }
@@ -426,7 +478,8 @@ ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg
   const double l_log_q = hcfg->has_low_value_goals ? std::log(1.0 - (1.0 - hcfg->low_discount)) : 0.0;
   hipLaunchKernelGGL(hgc_sample_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, *buf,
                      *cfg, *hcfg, cc, num_cols, total, (int)tile, dr, k0, k1, (uint32_t)call_index,
-                     (uint32_t)(call_index >> 32), v_log_q, a_log_q, l_log_q, *out, rec);
+                     (uint32_t)(call_index >> 32), v_log_q, a_log_q, l_log_q, *out, rec,
+                     tile <= 4 && flat4_columns(cc, num_cols));
   OGBX_LAUNCHED("hgc_sample_kernel");
   return OGBX_OK;
 }

@@ -48,6 +48,7 @@ class GcBuffer(ctypes.Structure):
         ('valid_idxs', ctypes.c_void_p),
         ('num_valid', ctypes.c_int64),
         ('traj_end', ctypes.c_void_p),
+        ('valid_traj_end', ctypes.c_void_p),
     ]
 
 
@@ -231,8 +232,11 @@ class GCDataset:
         else:
             self.traj_end.fill_(self.size - 1)
         valid = getattr(dataset, 'valid_idxs', None)
+        # trajectory end of every valid row: the drawn index and its end load in parallel
+        self.valid_traj_end = self.traj_end[valid].contiguous() if valid is not None else None
         self._buf = GcBuffer(self.size, valid.data_ptr() if valid is not None else None,
-                             valid.numel() if valid is not None else 0, self.traj_end.data_ptr())
+                             valid.numel() if valid is not None else 0, self.traj_end.data_ptr(),
+                             self.valid_traj_end.data_ptr() if valid is not None else None)
         self._valid = valid
 
         def thresh(p_traj, p_cur):
