@@ -359,7 +359,7 @@ ogbx_status ogbx_nonzero_f32(const float* x, int64_t n, int64_t* out, int64_t* c
                              void* stream);
 
 /* ======================================================================
- * Powderworld (batched PowderworldEnv in 'task' mode, easy element set)
+ * Powderworld (batched PowderworldEnv in 'task' mode; easy, medium, hard)
  * Reference: ogbench/powderworld/powderworld_env.py:21-476, sim.py:15-590,
  * registration ogbench/powderworld/__init__.py:3-8 (max_episode_steps 500).
  * One env = one world_size^2 grid; state stays in HBM between calls.
@@ -371,38 +371,48 @@ typedef struct {
   int32_t world_size;        /* 32 or 64 (PowderworldEnv world_size, :24) */
   int32_t grid_size;         /* 4 (:25) */
   int32_t brush_size;        /* 4 (:26) */
-  int32_t num_elems;         /* 2 = easy; 5/8 (medium/hard) -> OGBX_EINVAL for now */
+  int32_t num_elems;         /* 2 = easy, 5 = medium, 8 = hard (:57-62) */
   int32_t max_episode_steps; /* TimeLimit (500 in the registry) */
   int32_t pad;
 } ogbx_powder_opts;
 
-/* PowderworldEnv.__init__ (+ set_tasks, :81-282): the goal world of every task
- * is replayed once on the device at create. */
+/* PowderworldEnv.__init__ (+ set_tasks, :81-282).  Easy: the goal world of
+ * every task is replayed once on the device at create (its forward is
+ * deterministic).  Medium/hard: the forward is stochastic, so every reset
+ * replays its env's goal (powderworld_env.py:320-329) and keeps it per env. */
 ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int32_t device,
                                ogbx_powder_t* out);
 ogbx_status ogbx_powder_destroy(ogbx_powder_t env);
 ogbx_status ogbx_powder_describe(ogbx_powder_t env, int32_t* world_size, int32_t* xy_action_size,
                                  int32_t* num_elems, int32_t* num_tasks, int32_t* tol);
-/* Goal world element ids, host uint8 [num_tasks, H, W] (cur_goal_world, :329). */
+/* Goal world element ids, host uint8 [num_tasks, H, W] (cur_goal_world, :329);
+ * easy only (medium/hard goals: ogbx_powder_full_state). */
 ogbx_status ogbx_powder_goal_worlds(ogbx_powder_t env, uint8_t* out);
 
 /* PowderworldEnv.reset (:284-352) for envs with mask[e] != 0 (mask NULL = all).
  * task_id: device int32 [N] in 1..num_tasks, NULL = random task per env.
  * reset_action: device int32 [N,3] (elem index, x, y) of the random initial
  * semantic action (sample_semantic_action, :446-451), NULL = Philox draws.
+ * rand (medium/hard): device float32 [N, rand_rows, 3, H, W], the three rand
+ * fields (rand_movement, rand_interact, rand_element; sim.py:363-380) of each
+ * forward: row s < len(task) = goal action s, row len(task) = the reset's
+ * forward.  NULL = Philox.  Needs task_id, reset_action and rand_rows >=
+ * longest task + 1.
  * obs, goal_obs: device uint8 [N, H, W, 6] (ob and info['goal']). */
 ogbx_status ogbx_powder_reset(ogbx_powder_t env, const int32_t* task_id, const uint8_t* mask,
-                              const int32_t* reset_action, uint8_t* obs, uint8_t* goal_obs,
-                              uint64_t seed, void* stream);
+                              const int32_t* reset_action, const float* rand, int32_t rand_rows,
+                              uint8_t* obs, uint8_t* goal_obs, uint64_t seed, void* stream);
 
 /* k_steps x PowderworldEnv.step (:354-427) under TimeLimit.  action: device
  * int32 [k_steps, N]; an action outside the stage's range takes a random one
  * (np.random.randint, :358-377): draws[k, N] supplies those values, NULL =
- * Philox.  Outputs per (k, env): obs uint8 [k,N,H,W,6], reward float32,
- * terminated/truncated/success uint8.  auto_reset != 0 resets done envs in the
- * same step (obs is then the new episode's first observation). */
+ * Philox.  rand (medium/hard): device float32 [k_steps, N, 3, H, W] rand
+ * fields of the forward of each third step, NULL = Philox (auto-resets always
+ * draw from Philox).  Outputs per (k, env): obs uint8 [k,N,H,W,6], reward
+ * float32, terminated/truncated/success uint8.  auto_reset != 0 resets done
+ * envs in the same step (obs is then the new episode's first observation). */
 ogbx_status ogbx_powder_step(ogbx_powder_t env, const int32_t* action, int32_t k_steps,
-                             const int32_t* draws, uint8_t* obs, float* reward,
+                             const int32_t* draws, const float* rand, uint8_t* obs, float* reward,
                              uint8_t* terminated, uint8_t* truncated, uint8_t* success,
                              int32_t auto_reset, void* stream);
 
@@ -413,10 +423,30 @@ ogbx_status ogbx_powder_step(ogbx_powder_t env, const int32_t* action, int32_t k
 ogbx_status ogbx_powder_state(ogbx_powder_t env, uint8_t** world, int32_t** ctrl,
                               int32_t** elapsed, uint32_t** episode);
 
-/* `steps` x PWSim.forward (sim.py:363-380) on packed worlds, device uint8
- * [n_worlds, H*W] in -> out (may alias). */
+/* Medium/hard state: momentum int8 [N, H*W] (channel 6), velocity float32
+ * [N, H*W, 2] (channels 3, 4), goal ids uint8 [N, H*W] (cur_goal_world). */
+ogbx_status ogbx_powder_full_state(ogbx_powder_t env, int8_t** momentum, float** velocity,
+                                   uint8_t** goal_ids);
+
+/* `steps` x PWSim.forward (sim.py:363-380) on packed easy worlds, device
+ * uint8 [n_worlds, H*W] in -> out (may alias). */
 ogbx_status ogbx_powder_forward(ogbx_powder_t env, const uint8_t* world_in, int64_t n_worlds,
                                 int32_t steps, uint8_t* world_out, void* stream);
+
+/* `steps` x PWSim.forward with every rule (stone, gravity, sand, fluid, ice,
+ * water, fire, plant, velocity; sim.py:284-308, 461-982) on worlds in the
+ * reference's layout, device float32 [n_worlds, 9, H, W] in -> out.  rand:
+ * device float32 [steps, n_worlds, 3, H, W] or NULL (Philox).  rgb_out
+ * (optional): PWRenderer.render of the result, uint8 [n_worlds, H, W, 3]. */
+ogbx_status ogbx_powder_forward_full(ogbx_powder_t env, const float* world_in, int64_t n_worlds,
+                                     int32_t steps, const float* rand, float* world_out,
+                                     uint8_t* rgb_out, void* stream);
+
+/* Task table (host only, no device): semantic actions (elem index, x, y) of
+ * task task_id (1-based) for num_elems 2/5/8 into seq [cap, 3], its length
+ * and success tolerance (set_tasks, powderworld_env.py:81-282). */
+ogbx_status ogbx_powder_task_table(int32_t num_elems, int32_t task_id, int32_t* seq, int32_t cap,
+                                   int32_t* len, int32_t* tol);
 
 /* ======================================================================
  * Dataset loader and relabel pass (ogbench/utils.py:14-96,

@@ -90,14 +90,22 @@ _SIGNATURES = {
     'ogbx_powder_destroy': (c_int32, [c_void_p]),
     'ogbx_powder_describe': (c_int32, [c_void_p, P(c_int32), P(c_int32), P(c_int32), P(c_int32), P(c_int32)]),
     'ogbx_powder_goal_worlds': (c_int32, [c_void_p, c_void_p]),
-    'ogbx_powder_reset': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    'ogbx_powder_reset': (
+        c_int32,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_uint64, c_void_p],
+    ),
     'ogbx_powder_step': (
         c_int32,
-        [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
-         c_void_p],
+        [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_int32, c_void_p],
     ),
     'ogbx_powder_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p)]),
+    'ogbx_powder_full_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p)]),
     'ogbx_powder_forward': (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    'ogbx_powder_forward_full': (
+        c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]
+    ),
+    'ogbx_powder_task_table': (c_int32, [c_int32, c_int32, c_void_p, c_int32, P(c_int32), P(c_int32)]),
     # evaluation
     'ogbx_eval_accumulate': (
         c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]

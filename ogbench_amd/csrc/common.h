@@ -91,6 +91,7 @@ enum StreamTag : uint32_t {
   kTagMazeGoal = 0x4D5A0004u,
   kTagPowderReset = 0x50570001u,
   kTagPowderAction = 0x50570002u,
+  kTagPowderRand = 0x50570003u,
   kTagGcSample = 0x47430001u,
   kTagHgcSample = 0x47430002u,
 };

@@ -68,6 +68,7 @@ __device__ __forceinline__ uint32_t rd(uint32_t v) { return (v & kGrav) ? (v & ~
 
 struct PowderParams {
   int32_t H, W, grid, brush, xy_size, num_elems, num_tasks, max_steps, tol;
+  int32_t tol_task[kPwMaxTasks];  // success tolerance per task
   int32_t elem_ids[8];           // _elems: element id per element index
   uint32_t lut[32];              // render colour of each id, R | G<<8 | B<<16
   int32_t seq_len[kPwMaxTasks];  // goal replay sequences (elem idx, x, y)
@@ -79,6 +80,10 @@ struct PowderState {
   int32_t* ctrl;
   int32_t* elapsed;
   uint32_t* episode;
+  // medium / hard only
+  int8_t* mom;       // [N, H*W] fluid momentum (channel 6)
+  float2* vel;       // [N, H*W] velocity (channels 3, 4)
+  uint8_t* goal_env; // [N, H*W] goal ids (the goal replay is stochastic)
 };
 
 template <int WS>
@@ -350,6 +355,12 @@ __device__ inline uint32_t pw_draw(uint64_t env, uint32_t ep, uint32_t slot, uin
   return bounded_u32(w.x, n);
 }
 
+}  // namespace ogbx
+
+#include "powder_full.h"
+
+namespace ogbx {
+
 // ---------------------------------------------------------------- kernels
 
 // Goal worlds: replay each task's semantic action sequence (one forward +
@@ -514,6 +525,208 @@ __global__ void __launch_bounds__(256) pw_forward_kernel(const PowderParams* __r
   store_seg(out + off, own);
 }
 
+
+// ============================================================ medium / hard
+// Full-rule worlds (powder_full.h): the state lives in LDS for the whole
+// launch; goal worlds are replayed per env (the forward is stochastic).
+
+template <int WS>
+__device__ __forceinline__ void pwf_tables(PwFullShared<WS>& sh, const PowderParams* __restrict__ Pp) {
+  const int t = threadIdx.x;
+  if (t < 32) sh.lut[t] = Pp->lut[t];
+  if (t < 8) sh.elem_ids[t] = Pp->elem_ids[t];
+  __syncthreads();
+}
+
+// Reset of one env (powderworld_env.py:284-344): replay the task's semantic
+// actions from the blank world (goal), keep its ids, optionally render the
+// goal observation, then blank + one forward + the initial brush paint.
+// rand: [rows, 3, H, W] injected fields (row s = goal action s, row len =
+// the reset's forward) or NULL = Philox.
+template <int WS>
+__device__ void pwf_reset_env(const FullWorld<WS>& fw, const PowderParams* __restrict__ Pp, int task, int elem,
+                              int x, int y, const float* __restrict__ rand, uint32_t r0, uint32_t r1, uint64_t e,
+                              uint32_t ep, uint8_t* __restrict__ goal_obs) {
+  constexpr int C = WS * WS;
+  const int grid = Pp->grid, brush = Pp->brush, len = Pp->seq_len[task - 1];
+  fw.blank();
+  for (int q = 0; q < len; ++q) {
+    const int8_t* a = Pp->seq[task - 1][q];
+    fw.forward_rand(rand ? rand + (size_t)q * 3 * C : nullptr, r0, r1, e, ep, kRandGoal | (uint32_t)q);
+    fw.paint(fw.s.elem_ids[a[0]], a[1] * grid, a[2] * grid, brush);
+  }
+  fw.keep_goal();
+  if (goal_obs) fw.observe(goal_obs, 0, 0u, 0, brush);
+  fw.blank();
+  fw.forward_rand(rand ? rand + (size_t)len * 3 * C : nullptr, r0, r1, e, ep, kRandStart);
+  fw.paint(fw.s.elem_ids[elem], x * grid, y * grid, brush);
+}
+
+template <int WS>
+__global__ void __launch_bounds__(256) pwf_reset_kernel(const PowderParams* __restrict__ Pp, PowderState S,
+                                                        const int32_t* __restrict__ task_id,
+                                                        const uint8_t* __restrict__ mask,
+                                                        const int32_t* __restrict__ reset_action,
+                                                        const float* __restrict__ rand, int32_t rand_rows,
+                                                        uint8_t* __restrict__ obs, uint8_t* __restrict__ goal_obs,
+                                                        uint32_t k0, uint32_t k1, uint32_t r0, uint32_t r1) {
+  constexpr int C = WS * WS;
+  __shared__ PwFullShared<WS> sh;
+  const int64_t e = blockIdx.x;
+  if (mask != nullptr && mask[e] == 0) return;
+  FullWorld<WS> fw(sh);
+  pwf_tables(sh, Pp);
+  const int ne = Pp->num_elems, xy = Pp->xy_size, nt = Pp->num_tasks;
+  const uint32_t ep = S.episode[e] + 1u;
+  int task = task_id ? task_id[e] : 1 + (int)pw_draw(e, ep, 0, k0, k1, (uint32_t)nt);
+  if (task < 1 || task > nt) task = 1;
+  int elem, x, y;
+  if (reset_action) {
+    elem = reset_action[3 * e], x = reset_action[3 * e + 1], y = reset_action[3 * e + 2];
+  } else {
+    elem = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
+    x = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
+    y = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+  }
+  pwf_reset_env(fw, Pp, task, elem, x, y, rand ? rand + (size_t)e * rand_rows * 3 * C : nullptr, r0, r1, e, ep,
+                goal_obs + (size_t)e * C * 6);
+#pragma unroll
+  for (int k = 0; k < FullWorld<WS>::CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
+  fw.store(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
+  const int errs = fw.errors();
+  fw.observe(obs + (size_t)e * C * 6, 0, 0u, 0, Pp->brush);
+  if (threadIdx.x == 0) {
+    S.ctrl[e] = (task << 16) | (errs < Pp->tol_task[task - 1] ? kCtrlSuccess : 0);
+    S.elapsed[e] = 0;
+    S.episode[e] = ep;
+  }
+}
+
+// k_steps env steps; rand: [k, N, 3, H, W] injected fields for the forward of
+// each third step, or NULL = Philox (auto-resets always use Philox).
+template <int WS>
+__global__ void __launch_bounds__(256) pwf_step_kernel(
+    const PowderParams* __restrict__ Pp, PowderState S, int64_t n, const int32_t* __restrict__ action,
+    const int32_t* __restrict__ draws, const float* __restrict__ rand, int32_t k_steps, uint8_t* __restrict__ obs,
+    float* __restrict__ reward, uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated,
+    uint8_t* __restrict__ success, int32_t auto_reset, uint32_t k0, uint32_t k1, uint32_t a0, uint32_t a1,
+    uint32_t r0, uint32_t r1) {
+  constexpr int C = WS * WS, CPT = FullWorld<WS>::CPT;
+  __shared__ PwFullShared<WS> sh;
+  FullWorld<WS> fw(sh);
+  const int64_t e = blockIdx.x;
+  pwf_tables(sh, Pp);
+  const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
+  const int max_steps = Pp->max_steps;
+  fw.load(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) sh.g[fw.cell(k)] = S.goal_env[(size_t)e * C + fw.cell(k)];
+  int ctrl = S.ctrl[e];
+  int el = S.elapsed[e];
+  uint32_t ep = S.episode[e];
+  const int task = (ctrl >> 16) & 255;
+  const int tol = Pp->tol_task[(task >= 1 && task <= Pp->num_tasks ? task : 1) - 1];
+  bool dirty = false, goal_dirty = false;
+  __syncthreads();
+  for (int k = 0; k < k_steps; ++k) {
+    const int64_t o = (int64_t)k * n + e;
+    const int act = action[o];
+    int stage = ctrl & 3, elem = (ctrl >> 2) & 63, x = (ctrl >> 8) & 255;
+    bool succ = (ctrl & kCtrlSuccess) != 0;
+    auto rnd = [&](int bound) -> int {
+      if (draws) return draws[o];
+      return (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)bound);
+    };
+    if (stage == 0) {
+      elem = act >= 0 && act < ne ? act : rnd(ne);
+    } else if (stage == 1) {
+      x = act >= 0 && act < xy ? act : rnd(xy);
+    } else {
+      const int y = act >= 0 && act < xy ? act : rnd(xy);
+      fw.forward_rand(rand ? rand + (size_t)o * 3 * C : nullptr, r0, r1, e, ep, kRandStep | (uint32_t)el);
+      fw.paint(sh.elem_ids[elem], x * grid, y * grid, brush);
+      succ = fw.errors() < tol;
+      dirty = true;
+    }
+    stage = stage == 2 ? 0 : stage + 1;
+    el += 1;
+    const bool trunc = el >= max_steps;
+    if (threadIdx.x == 0) {
+      reward[o] = succ ? 1.0f : 0.0f;
+      terminated[o] = succ;
+      truncated[o] = trunc;
+      success[o] = succ;
+    }
+    if (auto_reset && (succ || trunc)) {
+      ep += 1u;
+      const int re = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
+      const int rx = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
+      const int ry = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+      pwf_reset_env(fw, Pp, task, re, rx, ry, nullptr, r0, r1, e, ep, nullptr);
+      succ = fw.errors() < tol;
+      stage = 0;
+      el = 0;
+      dirty = goal_dirty = true;
+    }
+    ctrl = stage | (elem << 2) | (x << 8) | (ctrl & (255 << 16)) | (succ ? kCtrlSuccess : 0);
+    const uint32_t acol = sh.lut[sh.elem_ids[elem & 7] & 31];
+    fw.observe(obs + (size_t)o * C * 6, stage, acol, x * grid, brush);
+  }
+  if (dirty) fw.store(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
+  if (goal_dirty) {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
+  }
+  if (threadIdx.x == 0) {
+    S.ctrl[e] = ctrl;
+    S.elapsed[e] = el;
+    S.episode[e] = ep;
+  }
+}
+
+// Free-standing PWSim.forward on worlds in the reference's (n, 9, H, W)
+// float32 layout (tests / drop-in): rand [steps, n, 3, H, W] or NULL (Philox
+// keyed by the env seed); optional render of the result (n, H, W, 3).
+template <int WS>
+__global__ void __launch_bounds__(256) pwf_forward_kernel(const PowderParams* __restrict__ Pp,
+                                                          const float* __restrict__ in, int64_t n, int32_t steps,
+                                                          const float* __restrict__ rand, float* __restrict__ out,
+                                                          uint8_t* __restrict__ rgb, uint32_t r0, uint32_t r1) {
+  constexpr int C = WS * WS, CPT = FullWorld<WS>::CPT;
+  __shared__ PwFullShared<WS> sh;
+  FullWorld<WS> fw(sh);
+  const int64_t e = blockIdx.x;
+  pwf_tables(sh, Pp);
+  const float* w = in + (size_t)e * 9 * C;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int i = fw.cell(k);
+    const uint32_t id = (uint32_t)(int)w[i] & 31u;
+    sh.a[i] = (uint8_t)(id | (w[2 * C + i] != 0.0f ? kGrav : 0u) | (w[8 * C + i] > 0.0f ? kDidg : 0u));
+    sh.m[i] = (int8_t)(int)w[6 * C + i];
+    sh.v[i] = make_float2(w[3 * C + i], w[4 * C + i]);
+  }
+  __syncthreads();
+  for (int q = 0; q < steps; ++q)
+    fw.forward_rand(rand ? rand + ((size_t)q * n + e) * 3 * C : nullptr, r0, r1, e, 0u, kRandStep | (uint32_t)q);
+  float* d = out + (size_t)e * 9 * C;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int i = fw.cell(k);
+    const uint32_t a = sh.a[i];
+    d[i] = (float)fid(a);
+    d[C + i] = fdens(a);
+    d[2 * C + i] = (float)fgrav(a);
+    d[3 * C + i] = sh.v[i].x;
+    d[4 * C + i] = sh.v[i].y;
+    d[5 * C + i] = 0.0f;
+    d[6 * C + i] = (float)sh.m[i];
+    d[7 * C + i] = 0.0f;
+    d[8 * C + i] = (float)fdidg(a);
+  }
+  if (rgb) fw.observe(rgb + (size_t)e * C * 3, 0, 0u, 0, 0, true);
+}
+
 // Host-side task tables (powderworld_env.py:88-149), elem indices into
 // _elem_names = ['plant', 'stone'].
 static void easy_tasks(std::vector<std::vector<std::array<int, 3>>>& tasks) {
@@ -543,22 +756,134 @@ static void easy_tasks(std::vector<std::vector<std::array<int, 3>>>& tasks) {
   fill(tasks[4], STONE, 0);
 }
 
+
+// medium / hard tables (powderworld_env.py:150-280); element indices into
+// _elem_names = [sand, water, fire, plant, stone(, gas, wood, ice)].
+using PwSeq = std::vector<std::array<int, 3>>;
+static void pw_square(PwSeq& s, int elem, int x, int y, int size) {
+  for (int i = 0; i < size; ++i) s.push_back({elem, x + i, y + size - 1});
+  for (int i = size - 2; i >= 0; --i) s.push_back({elem, x, y + i});
+  for (int i = size - 2; i >= 0; --i) s.push_back({elem, x + size - 1, y + i});
+  for (int i = 1; i < size - 1; ++i) s.push_back({elem, x + i, y});
+}
+static void pw_fill(PwSeq& s, int elem) {
+  for (int y = 7; y >= 0; --y)
+    for (int x = 0; x < 8; ++x) s.push_back({elem, x, y});
+}
+static void full_tasks(int ne, std::vector<PwSeq>& t, std::vector<int>& tol) {
+  enum { SAND, WATER, FIRE, PLANT, STONE, GAS, WOOD, ICE };
+  t.assign(5, {});
+  if (ne == 5) {
+    pw_square(t[0], PLANT, 1, 1, 6);
+    pw_square(t[0], SAND, 0, 0, 8);
+    pw_square(t[0], STONE, 2, 2, 4);
+    pw_square(t[0], WATER, 3, 3, 2);
+    pw_fill(t[1], WATER);
+    pw_square(t[1], PLANT, 0, 0, 8);
+    pw_square(t[2], STONE, 0, 0, 8);
+    for (int i = 0; i < 32; ++i) t[2].push_back({SAND, 3, 1}), t[2].push_back({SAND, 4, 1});
+    for (int x = 0; x < 8; ++x) t[3].push_back({PLANT, x, 6});
+    for (int x = 0; x < 8; ++x) t[3].push_back({PLANT, x, 7});
+    for (int y = 7; y >= 0; --y) t[3].push_back({STONE, 0, y});
+    for (int y = 7; y >= 0; --y) t[3].push_back({STONE, 7, y});
+    for (int x = 1; x < 7; ++x) t[3].push_back({STONE, x, 4});
+    for (int x = 1; x < 7; ++x) t[3].push_back({STONE, x, 3});
+    pw_square(t[3], WATER, 2, 0, 3);
+    pw_square(t[3], WATER, 3, 0, 3);
+    for (int i = 0; i < 4; ++i) t[3].push_back({FIRE, 3, 7}), t[3].push_back({FIRE, 4, 7});
+    pw_fill(t[4], PLANT);
+    for (int y : {4, 7})
+      for (int x = 0; x < 8; ++x) t[4].push_back({WATER, x, y});
+    for (int i = 0; i < 2; ++i)
+      for (int x = 0; x < 8; ++x) t[4].push_back({FIRE, x, 0});
+    tol = {32, 64, 64, 64, 96};
+  } else {
+    pw_fill(t[0], SAND);
+    for (int x = 0; x < 8; ++x) t[0].push_back({SAND, x, 0});
+    for (int x = 0; x < 8; ++x) t[0].push_back({WATER, x, 7});
+    for (int x = 0; x < 8; ++x) t[0].push_back({GAS, x, 7});
+    for (int x = 0; x < 8; ++x) t[0].push_back({WATER, x, 7});
+    pw_square(t[1], WOOD, 0, 0, 8);
+    pw_square(t[1], PLANT, 1, 1, 6);
+    pw_square(t[1], GAS, 2, 2, 4);
+    for (int i = 0; i < 3; ++i)
+      for (int x = 0; x < 8; ++x) t[1].push_back({FIRE, x, 0});
+    for (int x = 0; x < 8; ++x) t[2].push_back({ICE, x, 0});
+    for (int y = 7; y >= 0; --y) t[2].push_back({STONE, 2, y});
+    for (int y = 7; y >= 0; --y) t[2].push_back({STONE, 5, y});
+    for (int y = 7; y > 0; --y) t[2].push_back({WATER, 3, y}), t[2].push_back({WATER, 4, y});
+    t[2].push_back({PLANT, 3, 3});
+    t[2].push_back({PLANT, 4, 3});
+    t[2].push_back({PLANT, 3, 4});
+    t[2].push_back({PLANT, 4, 4});
+    for (int y = 7; y > 0; --y)
+      for (int x : {0, 1, 6, 7}) t[2].push_back({GAS, x, y});
+    pw_square(t[3], PLANT, 1, 4, 3);
+    pw_square(t[3], WOOD, 4, 4, 3);
+    pw_square(t[3], ICE, 1, 1, 3);
+    pw_square(t[3], PLANT, 4, 1, 3);
+    for (int i = 0; i < 10; ++i) pw_square(t[3], PLANT, 4, 1, 3);
+    pw_fill(t[4], WATER);
+    pw_square(t[4], PLANT, 3, 3, 2);
+    for (int i = 0; i < 4; ++i) pw_square(t[4], STONE, 0, 0, 8);
+    pw_square(t[4], ICE, 3, 3, 2);
+    tol = {96, 96, 96, 64, 96};
+  }
+}
+
+static void task_tables(int ne, std::vector<PwSeq>& t, std::vector<int>& tol) {
+  if (ne == 2) {
+    easy_tasks(t);
+    tol.assign(t.size(), 32);
+  } else {
+    full_tasks(ne, t, tol);
+  }
+}
 }  // namespace ogbx
 
 struct ogbx_powder_env {
   int32_t device = 0;
   int64_t n = 0;
+  bool full = false;  // medium / hard element sets (full rule set)
+  int32_t max_seq = 0;
   ogbx::PowderParams P;
   ogbx::PowderParams* Pd = nullptr;
   ogbx::PowderState S{};
-  uint8_t* goals = nullptr;  // [num_tasks, H*W] goal ids
+  uint8_t* goals = nullptr;  // easy: [num_tasks, H*W] goal ids
   uint64_t seed = 0;
   bool was_reset = false;
 };
 
 using namespace ogbx;
 
+namespace {
+// dispatch a kernel template on the world size
+#define PW_LAUNCH(kern, e, grid, stream, ...)                                                  \
+  do {                                                                                         \
+    if ((e)->P.W == 64)                                                                        \
+      hipLaunchKernelGGL(kern<64>, dim3(grid), dim3(256), 0, (hipStream_t)(stream), __VA_ARGS__); \
+    else                                                                                       \
+      hipLaunchKernelGGL(kern<32>, dim3(grid), dim3(256), 0, (hipStream_t)(stream), __VA_ARGS__); \
+  } while (0)
+}  // namespace
+
 extern "C" {
+
+ogbx_status ogbx_powder_task_table(int32_t num_elems, int32_t task_id, int32_t* seq, int32_t cap,
+                                   int32_t* len, int32_t* tol) {
+  OGBX_CHECK(num_elems == 2 || num_elems == 5 || num_elems == 8, OGBX_EINVAL, "num_elems must be 2, 5 or 8");
+  std::vector<PwSeq> tasks;
+  std::vector<int> tols;
+  task_tables(num_elems, tasks, tols);
+  OGBX_CHECK(task_id >= 1 && task_id <= (int)tasks.size(), OGBX_EINVAL, "task_id out of range");
+  const PwSeq& t = tasks[task_id - 1];
+  if (len) *len = (int32_t)t.size();
+  if (tol) *tol = tols[task_id - 1];
+  if (seq)
+    for (int q = 0; q < (int)t.size() && q < cap; ++q)
+      for (int k = 0; k < 3; ++k) seq[3 * q + k] = t[q][k];
+  return OGBX_OK;
+}
 
 ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int32_t device,
                                ogbx_powder_t* out) {
@@ -567,10 +892,8 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
   OGBX_CHECK(n_envs > 0 && n_envs <= (1ll << 31), OGBX_EINVAL, "n_envs out of range");
   const int ws = opts->world_size;
   OGBX_CHECK(ws == 32 || ws == 64, OGBX_EINVAL, "world_size must be 32 or 64");
-  OGBX_CHECK(opts->num_elems == 2 || opts->num_elems == 5 || opts->num_elems == 8, OGBX_EINVAL,
-             "num_elems must be 2, 5 or 8");
-  OGBX_CHECK(opts->num_elems == 2, OGBX_EINVAL,
-             "only powderworld-easy (num_elems=2) dynamics are implemented");
+  const int ne = opts->num_elems;
+  OGBX_CHECK(ne == 2 || ne == 5 || ne == 8, OGBX_EINVAL, "num_elems must be 2, 5 or 8");
   OGBX_CHECK(opts->grid_size == 4 && opts->brush_size == 4, OGBX_EINVAL,
              "only the registered grid_size=4 / brush_size=4 are supported");
   OGBX_CHECK(opts->max_episode_steps > 0, OGBX_EINVAL, "max_episode_steps must be positive");
@@ -579,17 +902,18 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
   auto* e = new ogbx_powder_env();
   e->device = device;
   e->n = n_envs;
+  e->full = ne != 2;
   PowderParams& P = e->P;
   std::memset(&P, 0, sizeof(P));
   P.H = P.W = ws;
   P.grid = opts->grid_size;
   P.brush = opts->brush_size;
   P.xy_size = (ws - P.brush) / P.grid + 1;
-  P.num_elems = 2;
-  P.elem_ids[0] = 8;  // plant
-  P.elem_ids[1] = 9;  // stone
+  P.num_elems = ne;
+  // _elems (powderworld_env.py:57-62): element id per element index
+  static const int ids2[2] = {8, 9}, ids8[8] = {2, 3, 7, 8, 9, 4, 5, 6};
+  for (int k = 0; k < ne; ++k) P.elem_ids[k] = ne == 2 ? ids2[k] : ids8[k];
   P.max_steps = opts->max_episode_steps;
-  P.tol = 32;
   // render LUT: uint8(clip(float32(c)/255 * 1 + 0) * 255) (sim.py:402-453)
   static const int colors[21][3] = {
       {236, 240, 241}, {108, 122, 137}, {243, 194, 58}, {75, 119, 190}, {179, 157, 219},
@@ -604,13 +928,17 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
       v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
       P.lut[i] |= (uint32_t)(uint8_t)(v * 255.0f) << (8 * c);
     }
-  std::vector<std::vector<std::array<int, 3>>> tasks;
-  easy_tasks(tasks);
+  std::vector<PwSeq> tasks;
+  std::vector<int> tols;
+  task_tables(ne, tasks, tols);
   P.num_tasks = (int)tasks.size();
+  P.tol = tols[0];
   for (int t = 0; t < P.num_tasks; ++t) {
+    P.tol_task[t] = tols[t];
     P.seq_len[t] = (int)tasks[t].size();
-    for (size_t s = 0; s < tasks[t].size(); ++s)
-      for (int k = 0; k < 3; ++k) P.seq[t][s][k] = (int8_t)tasks[t][s][k];
+    e->max_seq = std::max(e->max_seq, P.seq_len[t]);
+    for (size_t q = 0; q < tasks[t].size(); ++q)
+      for (int k = 0; k < 3; ++k) P.seq[t][q][k] = (int8_t)tasks[t][q][k];
   }
   const size_t n = (size_t)n_envs, HW = (size_t)ws * ws;
   hipError_t h = hipMalloc(&e->Pd, sizeof(PowderParams));
@@ -619,17 +947,23 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
   if (h == hipSuccess) h = hipMalloc(&e->S.ctrl, n * sizeof(int32_t));
   if (h == hipSuccess) h = hipMalloc(&e->S.elapsed, n * sizeof(int32_t));
   if (h == hipSuccess) h = hipMalloc(&e->S.episode, n * sizeof(uint32_t));
-  if (h == hipSuccess) h = hipMalloc(&e->goals, (size_t)P.num_tasks * HW);
   if (h == hipSuccess) h = hipMemset(e->S.world, 0, n * HW);
   if (h == hipSuccess) h = hipMemset(e->S.ctrl, 0, n * sizeof(int32_t));
   if (h == hipSuccess) h = hipMemset(e->S.elapsed, 0, n * sizeof(int32_t));
   if (h == hipSuccess) h = hipMemset(e->S.episode, 0, n * sizeof(uint32_t));
-  if (h == hipSuccess) {
-    if (ws == 64)
-      hipLaunchKernelGGL(pw_goal_kernel<64>, dim3(P.num_tasks), dim3(256), 0, 0, e->Pd, e->goals);
-    else
-      hipLaunchKernelGGL(pw_goal_kernel<32>, dim3(P.num_tasks), dim3(256), 0, 0, e->Pd, e->goals);
-    h = hipGetLastError();
+  if (e->full) {
+    if (h == hipSuccess) h = hipMalloc(&e->S.mom, n * HW);
+    if (h == hipSuccess) h = hipMalloc(&e->S.vel, n * HW * sizeof(float2));
+    if (h == hipSuccess) h = hipMalloc(&e->S.goal_env, n * HW);
+    if (h == hipSuccess) h = hipMemset(e->S.mom, 0, n * HW);
+    if (h == hipSuccess) h = hipMemset(e->S.vel, 0, n * HW * sizeof(float2));
+    if (h == hipSuccess) h = hipMemset(e->S.goal_env, 0, n * HW);
+  } else {
+    if (h == hipSuccess) h = hipMalloc(&e->goals, (size_t)P.num_tasks * HW);
+    if (h == hipSuccess) {
+      PW_LAUNCH(pw_goal_kernel, e, P.num_tasks, 0, e->Pd, e->goals);
+      h = hipGetLastError();
+    }
   }
   if (h == hipSuccess) h = hipDeviceSynchronize();
   if (h != hipSuccess) {
@@ -648,6 +982,9 @@ ogbx_status ogbx_powder_destroy(ogbx_powder_t e) {
   (void)hipFree(e->S.ctrl);
   (void)hipFree(e->S.elapsed);
   (void)hipFree(e->S.episode);
+  (void)hipFree(e->S.mom);
+  (void)hipFree(e->S.vel);
+  (void)hipFree(e->S.goal_env);
   (void)hipFree(e->goals);
   delete e;
   return OGBX_OK;
@@ -666,6 +1003,8 @@ ogbx_status ogbx_powder_describe(ogbx_powder_t e, int32_t* world_size, int32_t* 
 
 ogbx_status ogbx_powder_goal_worlds(ogbx_powder_t e, uint8_t* out) {
   OGBX_CHECK(e && out, OGBX_EINVAL, "null argument");
+  OGBX_CHECK(!e->full, OGBX_EINVAL,
+             "medium/hard goal worlds are stochastic and per env (ogbx_powder_full_state goal_ids)");
   OGBX_HIP(hipSetDevice(e->device));
   OGBX_HIP(hipMemcpy(out, e->goals, (size_t)e->P.num_tasks * e->P.H * e->P.W,
                      hipMemcpyDeviceToHost));
@@ -673,45 +1012,53 @@ ogbx_status ogbx_powder_goal_worlds(ogbx_powder_t e, uint8_t* out) {
 }
 
 ogbx_status ogbx_powder_reset(ogbx_powder_t e, const int32_t* task_id, const uint8_t* mask,
-                              const int32_t* reset_action, uint8_t* obs, uint8_t* goal_obs,
-                              uint64_t seed, void* stream) {
+                              const int32_t* reset_action, const float* rand, int32_t rand_rows,
+                              uint8_t* obs, uint8_t* goal_obs, uint64_t seed, void* stream) {
   OGBX_CHECK(e && obs && goal_obs, OGBX_EINVAL, "ogbx_powder_reset: null argument");
+  OGBX_CHECK(rand == nullptr || e->full, OGBX_EINVAL, "rand fields apply to medium/hard worlds only");
+  OGBX_CHECK(rand == nullptr || (task_id != nullptr && reset_action != nullptr && rand_rows >= e->max_seq + 1),
+             OGBX_EINVAL, "injected rand needs task_id, reset_action and rand_rows >= longest task + 1");
   OGBX_HIP(hipSetDevice(e->device));
   e->seed = seed;
-  uint32_t k0, k1;
+  uint32_t k0, k1, r0, r1;
   seed_key(seed, kTagPowderReset, &k0, &k1);
-  if (e->P.W == 64)
-    hipLaunchKernelGGL(pw_reset_kernel<64>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
-                       e->Pd, e->S, e->goals, task_id, mask, reset_action, obs, goal_obs, k0, k1);
-  else
-    hipLaunchKernelGGL(pw_reset_kernel<32>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
-                       e->Pd, e->S, e->goals, task_id, mask, reset_action, obs, goal_obs, k0, k1);
-  OGBX_LAUNCHED("pw_reset_kernel");
+  seed_key(seed, kTagPowderRand, &r0, &r1);
+  if (e->full) {
+    PW_LAUNCH(pwf_reset_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, task_id, mask, reset_action, rand,
+              rand_rows, obs, goal_obs, k0, k1, r0, r1);
+    OGBX_LAUNCHED("pwf_reset_kernel");
+  } else {
+    PW_LAUNCH(pw_reset_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->goals, task_id, mask, reset_action,
+              obs, goal_obs, k0, k1);
+    OGBX_LAUNCHED("pw_reset_kernel");
+  }
   e->was_reset = true;
   return OGBX_OK;
 }
 
 ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_steps,
-                             const int32_t* draws, uint8_t* obs, float* reward,
+                             const int32_t* draws, const float* rand, uint8_t* obs, float* reward,
                              uint8_t* terminated, uint8_t* truncated, uint8_t* success,
                              int32_t auto_reset, void* stream) {
   OGBX_CHECK(e && action && obs && reward && terminated && truncated && success, OGBX_EINVAL,
              "ogbx_powder_step: null argument");
   OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
   OGBX_CHECK(k_steps >= 1, OGBX_EINVAL, "k_steps must be >= 1");
+  OGBX_CHECK(rand == nullptr || e->full, OGBX_EINVAL, "rand fields apply to medium/hard worlds only");
   OGBX_HIP(hipSetDevice(e->device));
-  uint32_t k0, k1, a0, a1;
+  uint32_t k0, k1, a0, a1, r0, r1;
   seed_key(e->seed, kTagPowderReset, &k0, &k1);
   seed_key(e->seed, kTagPowderAction, &a0, &a1);
-  if (e->P.W == 64)
-    hipLaunchKernelGGL(pw_step_kernel<64>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
-                       e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs, reward, terminated,
-                       truncated, success, auto_reset, k0, k1, a0, a1);
-  else
-    hipLaunchKernelGGL(pw_step_kernel<32>, dim3((uint32_t)e->n), dim3(256), 0, (hipStream_t)stream,
-                       e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs, reward, terminated,
-                       truncated, success, auto_reset, k0, k1, a0, a1);
-  OGBX_LAUNCHED("pw_step_kernel");
+  seed_key(e->seed, kTagPowderRand, &r0, &r1);
+  if (e->full) {
+    PW_LAUNCH(pwf_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps, obs,
+              reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1, r0, r1);
+    OGBX_LAUNCHED("pwf_step_kernel");
+  } else {
+    PW_LAUNCH(pw_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs,
+              reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1);
+    OGBX_LAUNCHED("pw_step_kernel");
+  }
   return OGBX_OK;
 }
 
@@ -726,19 +1073,38 @@ ogbx_status ogbx_powder_state(ogbx_powder_t e, uint8_t** world, int32_t** ctrl, 
   return OGBX_OK;
 }
 
+ogbx_status ogbx_powder_full_state(ogbx_powder_t e, int8_t** momentum, float** velocity, uint8_t** goal_ids) {
+  OGBX_CHECK(e, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->full, OGBX_EINVAL, "easy worlds carry no momentum / velocity / per-env goals");
+  if (momentum) *momentum = e->S.mom;
+  if (velocity) *velocity = reinterpret_cast<float*>(e->S.vel);
+  if (goal_ids) *goal_ids = e->S.goal_env;
+  return OGBX_OK;
+}
+
 ogbx_status ogbx_powder_forward(ogbx_powder_t e, const uint8_t* world_in, int64_t n_worlds,
                                 int32_t steps, uint8_t* world_out, void* stream) {
   OGBX_CHECK(e && world_in && world_out && n_worlds >= 0 && steps >= 0, OGBX_EINVAL,
              "ogbx_powder_forward: bad argument");
+  OGBX_CHECK(!e->full, OGBX_EINVAL, "packed-byte forward is the easy element set; use ogbx_powder_forward_full");
   if (n_worlds == 0) return OGBX_OK;
   OGBX_HIP(hipSetDevice(e->device));
-  if (e->P.W == 64)
-    hipLaunchKernelGGL(pw_forward_kernel<64>, dim3((uint32_t)n_worlds), dim3(256), 0,
-                       (hipStream_t)stream, e->Pd, world_in, world_out, steps);
-  else
-    hipLaunchKernelGGL(pw_forward_kernel<32>, dim3((uint32_t)n_worlds), dim3(256), 0,
-                       (hipStream_t)stream, e->Pd, world_in, world_out, steps);
+  PW_LAUNCH(pw_forward_kernel, e, (uint32_t)n_worlds, stream, e->Pd, world_in, world_out, steps);
   OGBX_LAUNCHED("pw_forward_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_powder_forward_full(ogbx_powder_t e, const float* world_in, int64_t n_worlds, int32_t steps,
+                                     const float* rand, float* world_out, uint8_t* rgb_out, void* stream) {
+  OGBX_CHECK(e && world_in && world_out && n_worlds >= 0 && steps >= 0, OGBX_EINVAL,
+             "ogbx_powder_forward_full: bad argument");
+  if (n_worlds == 0) return OGBX_OK;
+  OGBX_HIP(hipSetDevice(e->device));
+  uint32_t r0, r1;
+  seed_key(e->seed, kTagPowderRand, &r0, &r1);
+  PW_LAUNCH(pwf_forward_kernel, e, (uint32_t)n_worlds, stream, e->Pd, world_in, n_worlds, steps, rand, world_out,
+            rgb_out, r0, r1);
+  OGBX_LAUNCHED("pwf_forward_kernel");
   return OGBX_OK;
 }
 

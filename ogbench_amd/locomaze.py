@@ -506,7 +506,8 @@ def _from_ptr(addr, shape, dtype, device):
     nbytes = numel * torch.empty((), dtype=dtype).element_size()
     iface = {
         'shape': tuple(shape),
-        'typestr': {torch.float64: '<f8', torch.int32: '<i4', torch.uint8: '|u1', torch.float32: '<f4'}[dtype],
+        'typestr': {torch.float64: '<f8', torch.int32: '<i4', torch.uint8: '|u1', torch.int8: '|i1',
+                    torch.float32: '<f4'}[dtype],
         'data': (addr, False),
         'version': 3,
         'strides': None,

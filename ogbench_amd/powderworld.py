@@ -17,7 +17,13 @@ Differences that follow from batching (documented in DESIGN.md):
     counter-based Philox stream keyed by ``seed``; they can be injected
     exactly (``options['reset_action']``, ``step(..., draws=...)``) for parity
     tests.
-  * only the 'easy' element set (num_elems=2) is implemented so far.
+  * medium/hard (num_elems 5/8) run every rule of PWSim (sand, fluids, ice,
+    water, fire, plant, velocity); their forward draws three float32 rand
+    fields per call, which come from Philox on the device and can be
+    injected exactly (``options['rand']``, ``step(..., rand=...)``,
+    ``forward_full(..., rand=...)``).  Their goal worlds are replayed per env
+    at every reset (the forward is stochastic) and kept on the device
+    (``goal_ids()``).
 """
 
 from __future__ import annotations
@@ -26,7 +32,7 @@ import numpy as np
 
 from . import _lib
 from .locomaze import _from_ptr, _resolve_device, _torch, _zero_episodes
-from .powder_tasks import EASY_TASK_NAMES, easy_task_sequences
+from .powder_tasks import task_names, task_sequences, task_tols
 from .spaces import Box, Discrete
 
 ELEM_NAMES = {2: ['plant', 'stone'],
@@ -56,8 +62,6 @@ class PowderworldEnv:
             raise NotImplementedError("only mode='task' is implemented (data collection runs on the host)")
         if num_elems not in ELEM_NAMES:
             raise ValueError(f'num_elems must be one of {sorted(ELEM_NAMES)}')
-        if num_elems != 2:
-            raise NotImplementedError('only powderworld-easy (num_elems=2) dynamics are implemented')
         torch = _torch()
         self.device = _resolve_device(device)
         self.num_envs = int(num_envs)
@@ -87,13 +91,13 @@ class PowderworldEnv:
         self._xy_action_size = xy.value
         self.num_tasks = nt.value
         self._tol = tol.value
-        seqs = easy_task_sequences()
+        self._full = self._num_elems != 2
+        seqs, names, tols = task_sequences(num_elems), task_names(num_elems), task_tols(num_elems)
         self.task_infos = [
-            dict(task_name=EASY_TASK_NAMES[i],
-                 action_seq=[(self._elem_names[e], x, y) for e, x, y in seqs[i]],
-                 tol=self._tol)
+            dict(task_name=names[i], action_seq=[(self._elem_names[e], x, y) for e, x, y in seqs[i]], tol=tols[i])
             for i in range(self.num_tasks)
         ]
+        self._max_seq = max(len(q) for q in seqs)
 
         H = W = self._world_size
         self.single_observation_space = Box(0, 255, (H, W, 6), np.uint8)
@@ -133,7 +137,11 @@ class PowderworldEnv:
 
     # ------------------------------------------------------------ state
     def goal_worlds(self):
-        """Element ids of every task's goal world, uint8 [num_tasks, H, W] (host)."""
+        """Element ids of every task's goal world, uint8 [num_tasks, H, W] (host).
+
+        Easy only: medium/hard goals are stochastic and per env (goal_ids())."""
+        if self._full:
+            raise ValueError('medium/hard goal worlds are replayed per env at reset; use goal_ids()')
         H = W = self._world_size
         out = np.zeros((self.num_tasks, H, W), np.uint8)
         _lib.check(self._L.ogbx_powder_goal_worlds(self._h, out.ctypes.data_as(_lib.c_void_p)))
@@ -149,6 +157,42 @@ class PowderworldEnv:
                 _from_ptr(e.value, (n,), torch.int32, self.device),
                 _from_ptr(ep.value, (n,), torch.int32, self.device))
 
+    def _full_views(self):
+        torch = _torch()
+        m, v, g = (_lib.c_void_p() for _ in range(3))
+        _lib.check(self._L.ogbx_powder_full_state(self._h, m, v, g))
+        n, H = self.num_envs, self._world_size
+        return (_from_ptr(m.value, (n, H, H), torch.int8, self.device),
+                _from_ptr(v.value, (n, H, H, 2), torch.float32, self.device),
+                _from_ptr(g.value, (n, H, H), torch.uint8, self.device))
+
+    def goal_ids(self):
+        """Goal element ids per env, uint8 [N, H, W] (reference cur_goal_world)."""
+        if self._full:
+            return self._full_views()[2]
+        torch = _torch()
+        g = torch.as_tensor(self.goal_worlds(), device=self.device)
+        return g[(self.cur_task_ids.long() - 1).clamp(min=0)]
+
+    def world_full(self):
+        """Worlds in the reference's (N, 9, H, W) float32 layout."""
+        torch = _torch()
+        w = self._state_views()[0]
+        ids = (w & 31).long()
+        dens = torch.tensor([1, 4, 3, 2, 0, 4, 4, 0, 4, 3, 3, 2, 2, 4, 2, 4, 3, 3, 3, 4, 3, 0, 0, 0, 0, 0, 0, 0, 0,
+                             0, 0, 0], dtype=torch.float32, device=self.device)
+        out = torch.zeros(self.num_envs, 9, *w.shape[1:], dtype=torch.float32, device=self.device)
+        out[:, 0] = ids.float()
+        out[:, 1] = dens[ids]
+        out[:, 2] = ((w >> 5) & 1).float()
+        out[:, 8] = ((w >> 6) & 1).float()
+        if self._full:
+            m, v, _ = self._full_views()
+            out[:, 3] = v[..., 0]
+            out[:, 4] = v[..., 1]
+            out[:, 6] = m.float()
+        return out
+
     def world_ids(self):
         """Element id of every cell, uint8 [N, H, W] (reference self._world[:, 0])."""
         return self._state_views()[0] & 31
@@ -159,7 +203,11 @@ class PowderworldEnv:
 
     def state_dict(self):
         w, c, e, ep = self._state_views()
-        return dict(world=w.clone(), ctrl=c.clone(), elapsed=e.clone(), episode=ep.clone(), seed=self._seed)
+        sd = dict(world=w.clone(), ctrl=c.clone(), elapsed=e.clone(), episode=ep.clone(), seed=self._seed)
+        if self._full:
+            m, v, g = self._full_views()
+            sd.update(momentum=m.clone(), velocity=v.clone(), goal=g.clone())
+        return sd
 
     def load_state_dict(self, sd):
         w, c, e, ep = self._state_views()
@@ -170,15 +218,53 @@ class PowderworldEnv:
             ep.copy_(sd['episode'])
         if sd.get('seed') is not None:
             self._seed = int(sd['seed'])
+        if self._full:
+            m, v, g = self._full_views()
+            m.copy_(sd['momentum'])
+            v.copy_(sd['velocity'])
+            g.copy_(sd['goal'])
 
     def forward(self, worlds, steps=1):
         """PWSim.forward (sim.py:363-380) on packed worlds uint8 [n, H, W]."""
         torch = _torch()
+        if self._full:
+            raise ValueError('medium/hard worlds carry velocity and momentum; use forward_full')
         w = torch.as_tensor(worlds).to(self.device, torch.uint8).contiguous()
         out = torch.empty_like(w)
         _lib.check(self._L.ogbx_powder_forward(self._h, _lib.ptr(w), w.shape[0], int(steps), _lib.ptr(out),
                                                self._stream()))
         return out
+
+    def forward_full(self, worlds, steps=1, rand=None, render=False):
+        """PWSim.forward with every rule on (n, 9, H, W) float32 worlds.
+
+        rand: float32 [steps, n, 3, H, W] (rand_movement, rand_interact,
+        rand_element per forward) or None (Philox).  render: also return
+        PWRenderer.render of the result, uint8 [n, H, W, 3]."""
+        torch = _torch()
+        w = torch.as_tensor(worlds).to(self.device, torch.float32).contiguous()
+        n, H = w.shape[0], self._world_size
+        assert tuple(w.shape[1:]) == (9, H, H), f'worlds must be (n, 9, {H}, {H})'
+        r = None
+        if rand is not None:
+            r = torch.as_tensor(rand).to(self.device, torch.float32).contiguous()
+            assert tuple(r.shape) == (int(steps), n, 3, H, H), 'rand must be [steps, n, 3, H, W]'
+        out = torch.empty_like(w)
+        img = torch.empty(n, H, H, 3, dtype=torch.uint8, device=self.device) if render else None
+        _lib.check(self._L.ogbx_powder_forward_full(self._h, _lib.ptr(w), n, int(steps), _lib.ptr(r), _lib.ptr(out),
+                                                    _lib.ptr(img), self._stream()), 'forward_full')
+        return (out, img) if render else out
+
+    def _rand(self, rand, shape):
+        if rand is None:
+            return None
+        if not self._full:
+            raise ValueError('rand fields apply to medium/hard worlds only')
+        torch = _torch()
+        r = torch.as_tensor(rand).to(self.device, torch.float32).contiguous()
+        if tuple(r.shape) != shape:
+            raise ValueError(f'rand must have shape {shape}, got {tuple(r.shape)}')
+        return r
 
     # ------------------------------------------------------------ reset/step
     def reset(self, *, seed=None, options=None, mask=None):
@@ -186,7 +272,9 @@ class PowderworldEnv:
 
         options: ``task_id`` (int or [N] tensor), ``reset_action`` ([N,3]
         (elem index, x, y) of the random initial semantic action; test hook),
-        ``render_goal`` (unsupported).  Returns (obs [N,H,W,6] u8, {'goal': ...}).
+        ``rand`` (medium/hard test hook: float32 [N, R, 3, H, W] rand fields,
+        row s < len(task) for goal action s, row len(task) for the reset's
+        forward, R >= longest task + 1), ``render_goal`` (unsupported).  Returns (obs [N,H,W,6] u8, {'goal': ...}).
         """
         torch = _torch()
         options = {} if options is None else options
@@ -223,9 +311,14 @@ class PowderworldEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask).to(self.device, torch.uint8).contiguous()
+        rand, rows = options.get('rand'), 0
+        if rand is not None:
+            rows = int(np.shape(rand)[1])
+            H = self._world_size
+            rand = self._rand(rand, (self.num_envs, rows, 3, H, H))
         _lib.check(
-            self._L.ogbx_powder_reset(self._h, _lib.ptr(task_t), _lib.ptr(m), _lib.ptr(ra), _lib.ptr(self._obs),
-                                      _lib.ptr(self._goal), self._seed, self._stream()),
+            self._L.ogbx_powder_reset(self._h, _lib.ptr(task_t), _lib.ptr(m), _lib.ptr(ra), _lib.ptr(rand), rows,
+                                      _lib.ptr(self._obs), _lib.ptr(self._goal), self._seed, self._stream()),
             'reset',
         )
         return self._obs, {'goal': self._goal}
@@ -239,16 +332,20 @@ class PowderworldEnv:
             raise ValueError(f'action must have shape {shape}, got {tuple(action.shape)}')
         return action
 
-    def step(self, action, draws=None):
+    def step(self, action, draws=None, rand=None):
         """One PowderworldEnv.step (powderworld_env.py:354-427) + TimeLimit for all envs.
 
         action: int [N].  draws: optional int [N] replacement values for
         invalid actions (the reference's np.random.randint; test hook).
+        rand: medium/hard test hook, float32 [N, 3, H, W] rand fields of this
+        step's forward (used by envs at their third action step).
         """
         a = self._actions(action, (self.num_envs,))
         d = None if draws is None else self._actions(draws, (self.num_envs,))
+        H = self._world_size
+        r = self._rand(rand, (self.num_envs, 3, H, H))
         _lib.check(
-            self._L.ogbx_powder_step(self._h, _lib.ptr(a), 1, _lib.ptr(d), _lib.ptr(self._obs),
+            self._L.ogbx_powder_step(self._h, _lib.ptr(a), 1, _lib.ptr(d), _lib.ptr(r), _lib.ptr(self._obs),
                                      _lib.ptr(self._reward), _lib.ptr(self._term), _lib.ptr(self._trunc),
                                      _lib.ptr(self._succ), int(self.auto_reset), self._stream()),
             'step',
@@ -257,13 +354,14 @@ class PowderworldEnv:
         info = {'success': self._succ.view(torch.bool)}
         return self._obs, self._reward, self._term.view(torch.bool), self._trunc.view(torch.bool), info
 
-    def rollout(self, actions, draws=None, out=None):
+    def rollout(self, actions, draws=None, out=None, rand=None):
         """K fused steps in ONE launch: actions [K,N] -> per-step outputs [K,N,...]."""
         torch = _torch()
         K = int(np.shape(actions)[0])
         a = self._actions(actions, (K, self.num_envs))
         d = None if draws is None else self._actions(draws, (K, self.num_envs))
         H = self._world_size
+        r = self._rand(rand, (K, self.num_envs, 3, H, H))
         if out is None:
             kw = dict(device=self.device)
             out = dict(
@@ -274,7 +372,7 @@ class PowderworldEnv:
                 success=torch.empty(K, self.num_envs, dtype=torch.uint8, **kw),
             )
         _lib.check(
-            self._L.ogbx_powder_step(self._h, _lib.ptr(a), K, _lib.ptr(d), _lib.ptr(out['obs']),
+            self._L.ogbx_powder_step(self._h, _lib.ptr(a), K, _lib.ptr(d), _lib.ptr(r), _lib.ptr(out['obs']),
                                      _lib.ptr(out['reward']), _lib.ptr(out['terminated']),
                                      _lib.ptr(out['truncated']), _lib.ptr(out['success']), int(self.auto_reset),
                                      self._stream()),

@@ -54,3 +54,19 @@ def test_create_without_gpu_fails_loudly():
     st = L.ogbx_maze_create(b'large', 16, 0, opts, h)
     assert st == _lib.OGBX_EDEVICE
     assert 'CPU fallback' in _lib.last_error() or 'device' in _lib.last_error()
+
+
+def test_powder_task_tables_match_reference():
+    """The C++ task tables (every element set) vs the reference's set_tasks."""
+    import os
+
+    gold = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'powder_full_golden.npz'))
+    L = _lib.lib()
+    for ne in (2, 5, 8):
+        for t in range(1, 6):
+            buf = np.zeros((256, 3), np.int32)
+            n, tol = ctypes.c_int32(), ctypes.c_int32()
+            assert L.ogbx_powder_task_table(ne, t, buf.ctypes.data_as(ctypes.c_void_p), 256, n, tol) == 0
+            assert np.array_equal(buf[:n.value], gold[f'tasks{ne}_{t}_seq']), (ne, t)
+            assert tol.value == int(gold[f'tasks{ne}_{t}_tol'])
+    assert L.ogbx_powder_task_table(5, 6, None, 0, None, None) != 0

@@ -1,0 +1,194 @@
+"""GPU parity: the medium/hard powderworld kernels (every PWSim rule, through
+the C-ABI) vs the reference's own outputs (tests/golden/powder_full_golden.npz,
+rand fields recorded and injected) and the NumPy oracle
+(oracle/powder_full_np.py) on seeded inputs.  Float32 velocities included, the
+bar is bit-exact: the kernels follow the reference op by op."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import ogbench_amd
+from oracle import powder_full_np as orc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), 'golden', 'powder_full_golden.npz')
+
+
+@pytest.fixture(scope='module')
+def gold():
+    return dict(np.load(GOLD))
+
+
+def _env(gpu, n, ne=5, size=32, **kw):
+    name = {5: 'powderworld-medium-v0', 8: 'powderworld-hard-v0'}[ne]
+    return ogbench_amd.make(name, num_envs=n, device=gpu, world_size=size, **kw)
+
+
+def _diff(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    bad = np.argwhere(a != b)
+    return f'{len(bad)} mismatches, first {bad[:5].tolist()}'
+
+
+@pytest.mark.parametrize('size', [32, 64])
+def test_forward_matches_reference(gpu, gold, size):
+    env = _env(gpu, 1, size=size)
+    w0, outs, rands = gold[f'full{size}_in'], gold[f'full{size}_out'], gold[f'full{size}_rand']
+    # one forward at a time from the reference's own inputs
+    w = w0
+    for t in range(outs.shape[0]):
+        got = env.forward_full(w, 1, rand=rands[t][None]).cpu().numpy()
+        assert np.array_equal(got, outs[t]), (t, _diff(got, outs[t]))
+        w = outs[t]
+    # all six chained in one launch
+    got = env.forward_full(w0, outs.shape[0], rand=rands).cpu().numpy()
+    assert np.array_equal(got, outs[-1]), _diff(got, outs[-1])
+
+
+def test_render_with_velocity(gpu, gold):
+    env = _env(gpu, 1)
+    out, img = env.forward_full(gold['render_vel_world'], 0, render=True)
+    assert np.array_equal(out.cpu().numpy(), gold['render_vel_world'])
+    got = img.cpu().numpy()[0]
+    assert np.array_equal(got, gold['render_vel_img']), _diff(got, gold['render_vel_img'])
+
+
+def _seeded_world(rng, n, size, ne):
+    """Random full worlds: elements of the set, walls on the border, random
+    velocities and momenta (the states a trajectory reaches)."""
+    elems = orc.ELEM_IDS[ne] + [0, 0, 0]
+    ids = rng.choice(elems, size=(n, size, size))
+    ids[:, 0, :] = ids[:, -1, :] = ids[:, :, 0] = ids[:, :, -1] = orc.WALL
+    w = orc.from_ids(ids)
+    w[:, 3:5] = (rng.randn(n, 2, size, size) * 2.5).astype(np.float32) * (rng.rand(n, 1, size, size) < 0.3)
+    w[:, 6] = rng.choice([-2, 0, 2], size=(n, size, size)) * np.isin(ids, orc.FLUIDS)
+    w[:, 8] = rng.rand(n, size, size) < 0.2
+    stone = ids == orc.STONE
+    w[:, 2] = np.where(stone, rng.rand(n, size, size) < 0.5, w[:, 2])
+    return w.astype(np.float32)
+
+
+@pytest.mark.parametrize('ne,size', [(5, 32), (8, 32), (8, 64)])
+def test_forward_matches_oracle_seeded(gpu, ne, size):
+    rng = np.random.RandomState(100 + ne + size)
+    n, steps = 3, 8
+    w = _seeded_world(rng, n, size, ne)
+    rand = rng.rand(steps, n, 3, size, size).astype(np.float32)
+    env = _env(gpu, 1, ne=ne, size=size)
+    got = env.forward_full(w, steps, rand=rand).cpu().numpy()
+    ref = w
+    for t in range(steps):
+        ref = orc.forward(ref, [rand[t][:, k] for k in range(3)])
+    assert np.array_equal(got, ref), _diff(got, ref)
+
+
+def _padded_reset_rand(env, r, task):
+    """[1, R, 3, H, W]: goal rows then the reset forward at row len(task)."""
+    H = env._world_size
+    rows = env._max_seq + 1
+    out = np.zeros((1, rows, 3, H, H), np.float32)
+    out[0, :r.shape[0]] = r
+    assert r.shape[0] == len(env.task_infos[task - 1]['action_seq']) + 1
+    return out
+
+
+@pytest.mark.parametrize('ne', [5, 8])
+def test_env_trace_matches_reference(gpu, gold, ne):
+    tag = f'env{ne}_tr0'
+    task = int(gold[f'{tag}_task'])
+    env = _env(gpu, 1, ne=ne)
+    ob, info = env.reset(seed=0, options=dict(task_id=task, reset_action=gold[f'{tag}_reset_action'][None],
+                                              rand=_padded_reset_rand(env, gold[f'{tag}_reset_rand'], task)))
+    assert np.array_equal(env.goal_ids()[0].cpu().numpy(), gold[f'{tag}_goal_world'])
+    assert np.array_equal(info['goal'][0].cpu().numpy(), gold[f'{tag}_goal_ob'])
+    assert np.array_equal(ob[0].cpu().numpy(), gold[f'{tag}_reset_ob'])
+    acts, rands = gold[f'{tag}_actions'], gold[f'{tag}_step_rand']
+    for t in range(len(acts)):
+        ob, rew, term, trunc, info = env.step([int(acts[t])], rand=rands[t][None])
+        assert np.array_equal(ob[0].cpu().numpy(), gold[f'{tag}_obs'][t]), (t, _diff(ob[0].cpu(), gold[f'{tag}_obs'][t]))
+        assert float(rew[0]) == gold[f'{tag}_reward'][t]
+    fw = env.world_full()[0].cpu().numpy()
+    assert np.array_equal(fw, gold[f'{tag}_final_world']), _diff(fw, gold[f'{tag}_final_world'])
+
+
+def test_env_fused_rollout_matches_steps(gpu, gold):
+    """K steps in one launch == K single-step launches (injected rands)."""
+    tag = 'env5_tr0'
+    task = int(gold[f'{tag}_task'])
+    acts, rands = gold[f'{tag}_actions'], gold[f'{tag}_step_rand']
+    opts = dict(task_id=task, reset_action=gold[f'{tag}_reset_action'][None])
+    a = _env(gpu, 1)
+    a.reset(seed=0, options=dict(opts, rand=_padded_reset_rand(a, gold[f'{tag}_reset_rand'], task)))
+    out = a.rollout(acts[:, None], rand=rands[:, None])
+    assert np.array_equal(out['obs'][:, 0].cpu().numpy(), gold[f'{tag}_obs'])
+    assert np.array_equal(a.world_full()[0].cpu().numpy(), gold[f'{tag}_final_world'])
+
+
+def _host_errors(world, goal):
+    match = np.zeros(goal.shape, bool)
+    for dx, dy in [(0, 0), (1, 0), (-1, 0), (0, 1), (0, -1)]:
+        match |= goal == np.roll(world, (dy, dx), axis=(0, 1))
+    return int((~match).sum())
+
+
+@pytest.mark.parametrize('ne,size', [(5, 32), (8, 64)])
+def test_philox_batch_consistency(gpu, ne, size):
+    """Philox-driven batch: every env's step is the oracle forward of its
+    previous state under SOME rand field -> check what is rand-independent:
+    determinism per seed, state restore, success == goal-match < tol, obs ==
+    oracle render of the state, goals differ across envs (stochastic replay)."""
+    n, K = 16, 24
+    env = _env(gpu, n, ne=ne, size=size)
+    tasks = torch.arange(n, device=gpu) % env.num_tasks + 1
+    env.reset(seed=7, options=dict(task_id=tasks))
+    goals = env.goal_ids().cpu().numpy()
+    assert len({g.tobytes() for g in goals}) > env.num_tasks  # per-env stochastic goals
+    sd = env.state_dict()
+    rng = np.random.RandomState(3)
+    acts = rng.randint(0, max(ne, env._xy_action_size) + 2, size=(K, n))  # some invalid -> Philox draws
+    outs = []
+    for t in range(K):
+        ob, rew, term, trunc, info = env.step(acts[t])
+        w = env.world_full().cpu().numpy()
+        tids = env.cur_task_ids.cpu().numpy()
+        for e in range(n):
+            ref = orc.render(w[e])
+            assert np.array_equal(ob[e, ..., :3].cpu().numpy(), ref)
+            err = _host_errors(w[e, 0].astype(np.uint8), goals[e])
+            assert bool(info['success'][e]) == (err < env.task_infos[tids[e] - 1]['tol'])
+        outs.append(ob.clone())
+    # same seed + restored state -> identical trajectory
+    env.load_state_dict(sd)
+    for t in range(K):
+        ob, *_ = env.step(acts[t])
+        assert torch.equal(ob, outs[t])
+
+
+def test_auto_reset_replays_goal(gpu):
+    """max_episode_steps truncation with auto_reset: the next episode has a
+    fresh goal replay (new Philox stream) and a fresh world."""
+    env = _env(gpu, 8, max_episode_steps=6, auto_reset=True)
+    env.reset(seed=11, options=dict(task_id=2))
+    g0 = env.goal_ids().clone()
+    for t in range(6):
+        ob, rew, term, trunc, info = env.step(np.full(8, t % 3, np.int64))
+    assert bool(trunc.all())
+    g1 = env.goal_ids()
+    assert not torch.equal(g0, g1)  # replayed with new randomness
+    assert int(env._state_views()[2].max()) == 0  # elapsed reset
+    # goal of task 2 (water fill + plant square) still looks like it
+    assert ((g1 == orc.PLANT).sum(dim=(1, 2)) > 20).all()
+
+
+def test_full_errors(gpu):
+    env = _env(gpu, 2)
+    with pytest.raises(ValueError):
+        env.goal_worlds()
+    with pytest.raises(ValueError):
+        env.forward(np.zeros((1, 32, 32), np.uint8))
+    easy = ogbench_amd.make('powderworld-easy-v0', num_envs=1, device=gpu)
+    with pytest.raises(ValueError):
+        easy.step([0], rand=np.zeros((1, 3, 32, 32), np.float32))

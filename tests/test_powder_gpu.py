@@ -227,8 +227,6 @@ def test_auto_reset_on_success(gpu):
 
 
 def test_errors(gpu):
-    with pytest.raises(NotImplementedError):
-        ogbench_amd.make('powderworld-medium-v0', num_envs=1, device=gpu)
     with pytest.raises(ValueError):
         _env(gpu, 1, 48)
     env = _env(gpu, 2)
