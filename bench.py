@@ -467,22 +467,27 @@ def cpu_baseline_gc(data, cfg, B, args):
                 sample=f'{n} batches of {B} on the 1M-row humanoid buffer ({dt:.1f} s)')
 
 
-def bench_powder(args, world, rank, dev):
-    """powderworld-easy-v0, 64x64 worlds, N=4096 envs per GPU (SURVEY.md section 8 row b).
-    A step = one env.step of all envs (one pw_step_kernel launch), uniformly random
-    valid actions for the current stage, task i%5+1, same-step auto-reset."""
+def bench_powder(args, world, rank, dev, level='easy'):
+    """powderworld-{level}-v0, 64x64 worlds, N=4096 envs per GPU (SURVEY.md section 8 row b;
+    medium/hard: section 8f).  A step = one env.step of all envs (one step-kernel launch),
+    uniformly random valid actions for the current stage, task i%5+1, same-step auto-reset
+    (medium/hard: the auto-reset replays the task's goal in the same launch, as the
+    reference's reset does)."""
     import ogbench_amd
 
     n = 4096 if args.num_envs == 65536 else args.num_envs
     size = 64
-    env = ogbench_amd.make('powderworld-easy-v0', num_envs=n, device=dev, world_size=size, auto_reset=True)
+    ne = {'easy': 2, 'medium': 5, 'hard': 8}[level]
+    full = ne != 2
+    kern = 'pwf_step_kernel' if full else 'pw_step_kernel'
+    env = ogbench_amd.make(f'powderworld-{level}-v0', num_envs=n, device=dev, world_size=size, auto_reset=True)
     task = (torch.arange(n, dtype=torch.int32, device=dev) % 5) + 1
     env.reset(seed=rank, options=dict(task_id=task))
     gen = torch.Generator(device=dev)
     gen.manual_seed(5 + 1000 * rank)
     ring = 3 * 32
     xy = env._xy_action_size
-    hi = torch.tensor([2 if i % 3 == 0 else xy for i in range(ring)], device=dev).view(ring, 1)
+    hi = torch.tensor([ne if i % 3 == 0 else xy for i in range(ring)], device=dev).view(ring, 1)
     actions = (torch.rand(ring, n, device=dev, generator=gen) * hi).to(torch.int32)
 
     def step(i):
@@ -496,7 +501,10 @@ def bench_powder(args, world, rank, dev):
     kern_ms = _per_launch_ms(step, min(steps, 201) - min(steps, 201) % 3 or 1, dev)
     # algorithmic bytes per env-step: obs write H*W*6, world read H*W, world
     # write H*W on one step in three, action 4, reward 4, flags 3, ctrl 16.
-    per_step = size * size * 6 + size * size + size * size / 3 + 27
+    # medium/hard add momentum (1 B) + velocity (8 B) per cell read and
+    # written like the world, and the per-env goal ids read (1 B per cell).
+    per_cell_state = 10 if full else 1
+    per_step = size * size * (6 + per_cell_state * (1 + 1 / 3) + (1 if full else 0)) + 27
     achieved = per_step * n / (kern_ms * 1e-3) / 1e9
     extra = {}
     K = 48
@@ -515,19 +523,20 @@ def bench_powder(args, world, rank, dev):
         extra = dict(fused_k48_steps_per_s=n * K * reps * world / fdt, fused_k48_kernel_ms=fk_ms,
                      fused_k48_achieved_GBs=per_step * n * K / (fk_ms * 1e-3) / 1e9)
     result = dict(
-        metric='env steps/sec, powderworld-easy-v0 64x64, N=4096 parallel envs per GPU',
+        metric=f'env steps/sec, powderworld-{level}-v0 64x64, N={n} parallel envs per GPU',
         value=value, unit='env_steps/s', n_gpus=world, steps=steps, warmup=args.warmup,
         ms_per_step=dt / steps * 1e3, higher_is_better=True, scaling='weak', vs_baseline=None,
-        dtype='u8', data='synthetic (uniform valid Discrete actions per stage; Philox resets)',
-        config=dict(workload='powderworld-easy-v0 world_size=64', num_envs_per_gpu=n, auto_reset=True,
+        dtype='f32+u8' if full else 'u8',
+        data='synthetic (uniform valid Discrete actions per stage; Philox resets' + (' and rand fields)' if full else ')'),
+        config=dict(workload=f'powderworld-{level}-v0 world_size=64', num_envs_per_gpu=n, auto_reset=True,
                     parallelism=f'env-shard x{world}'),
-        roofline=dict(bound='hbm', kernel='pw_step_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('pw_step_kernel', kern_ms), kernel_ms=kern_ms,
+        roofline=dict(bound='hbm', kernel=kern, achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic(kern, kern_ms), kernel_ms=kern_ms,
                       alg_bytes_per_launch=per_step * n),
         extra=extra,
     )
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result['cpu_baseline'] = cpu_baseline_powder(size, args)
+        result['cpu_baseline'] = cpu_baseline_powder_full(ne, size, args) if full else cpu_baseline_powder(size, args)
     env.close()
     return result
 
@@ -555,12 +564,41 @@ def cpu_baseline_powder(size, args):
                 sample=f'{n} single-env steps of powderworld-easy {size}x{size} ({dt:.1f} s)')
 
 
+def cpu_baseline_powder_full(ne, size, args):
+    """The NumPy oracle of the full rule set (kind 'port', 1 core): one env at a
+    time, random valid actions, rand fields from np.random as the reference."""
+    from oracle import powder_full_np as orc
+    from ogbench_amd.powder_tasks import task_sequences
+
+    rng = np.random.RandomState(0)
+    o = orc.Env(ne, size)
+    H = size
+
+    def rand():
+        return [rng.rand(H, H).astype(np.float32) for _ in range(3)]
+
+    seq = task_sequences(ne)[0]
+    goal = o.replay(seq[:8], [rand() for _ in seq[:8]])[0, 0].astype(np.uint8)  # a short goal replay
+    o.reset(goal, 0, 3, 3, rand())
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        a = rng.randint(0, ne if o.stage == 0 else o.xy)
+        o.step(int(a), rand())
+        o.errors()
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit='env_steps/s', cores=1, kind='port',
+                sample=f'{n} single-env steps of powderworld-{"medium" if ne == 5 else "hard"} {size}x{size} '
+                       f'({dt:.1f} s; goal replays excluded)')
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=100)
-    ap.add_argument('--workload', default='pointmaze', choices=['pointmaze', 'powder', 'gcsample', 'hgcsample'])
+    ap.add_argument('--workload', default='pointmaze',
+                    choices=['pointmaze', 'powder', 'powder-medium', 'powder-hard', 'gcsample', 'hgcsample'])
     ap.add_argument('--num-envs', type=int, default=65536)
     ap.add_argument('--ring', type=int, default=128)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -576,7 +614,9 @@ def main():
     import sys
 
     sys.path.insert(0, ROOT)
-    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, gcsample=bench_gcsample, hgcsample=bench_hgcsample)[args.workload]
+    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, gcsample=bench_gcsample, hgcsample=bench_hgcsample,
+              **{'powder-medium': lambda *a: bench_powder(*a, level='medium'),
+                 'powder-hard': lambda *a: bench_powder(*a, level='hard')})[args.workload]
     result = fn(args, world, rank, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -529,6 +529,14 @@ __global__ void __launch_bounds__(256) pw_forward_kernel(const PowderParams* __r
 // ============================================================ medium / hard
 // Full-rule worlds (powder_full.h): the state lives in LDS for the whole
 // launch; goal worlds are replayed per env (the forward is stochastic).
+// 1024 threads per 64x64 world, 256 per 32x32 (4 cells per thread).
+template <int WS>
+constexpr int pwf_nt() { return WS == 64 ? 1024 : 256; }
+#ifndef OGBX_PWF_WAVES
+#define OGBX_PWF_WAVES 4  // waves per SIMD the register budget is sized for
+#endif
+template <int WS>
+using FW = FullWorld<WS, pwf_nt<WS>()>;
 
 template <int WS>
 __device__ __forceinline__ void pwf_tables(PwFullShared<WS>& sh, const PowderParams* __restrict__ Pp) {
@@ -538,32 +546,37 @@ __device__ __forceinline__ void pwf_tables(PwFullShared<WS>& sh, const PowderPar
   __syncthreads();
 }
 
-// Reset of one env (powderworld_env.py:284-344): replay the task's semantic
-// actions from the blank world (goal), keep its ids, optionally render the
-// goal observation, then blank + one forward + the initial brush paint.
-// rand: [rows, 3, H, W] injected fields (row s = goal action s, row len =
-// the reset's forward) or NULL = Philox.
+// One forward + paint of a reset (powderworld_env.py:284-344): op q < len
+// replays goal action q of the task from the blank world; op len keeps the
+// goal ids (and renders the goal observation if asked), starts a blank world
+// and applies the initial random semantic action (elem, x, y).  rand: [rows,
+// 3, H, W] injected fields (row q) or NULL = Philox.  Kernels call this from
+// ONE loop so the forward is inlined once per kernel.
 template <int WS>
-__device__ void pwf_reset_env(const FullWorld<WS>& fw, const PowderParams* __restrict__ Pp, int task, int elem,
-                              int x, int y, const float* __restrict__ rand, uint32_t r0, uint32_t r1, uint64_t e,
-                              uint32_t ep, uint8_t* __restrict__ goal_obs) {
+__device__ __forceinline__ void pwf_reset_op(const FW<WS>& fw, const PowderParams* __restrict__ Pp, int task,
+                                             int q, int elem, int x, int y, const float* __restrict__ rand,
+                                             uint32_t r0, uint32_t r1, uint64_t e, uint32_t ep,
+                                             uint8_t* __restrict__ goal_obs) {
   constexpr int C = WS * WS;
   const int grid = Pp->grid, brush = Pp->brush, len = Pp->seq_len[task - 1];
-  fw.blank();
-  for (int q = 0; q < len; ++q) {
+  if (q == 0) fw.blank();
+  int pe = elem, px = x, py = y;
+  uint32_t slot = kRandStart;
+  if (q < len) {
     const int8_t* a = Pp->seq[task - 1][q];
-    fw.forward_rand(rand ? rand + (size_t)q * 3 * C : nullptr, r0, r1, e, ep, kRandGoal | (uint32_t)q);
-    fw.paint(fw.s.elem_ids[a[0]], a[1] * grid, a[2] * grid, brush);
+    pe = a[0], px = a[1], py = a[2];
+    slot = kRandGoal | (uint32_t)q;
+  } else {
+    fw.keep_goal();
+    if (goal_obs) fw.observe(goal_obs, 0, 0u, 0, brush);
+    fw.blank();
   }
-  fw.keep_goal();
-  if (goal_obs) fw.observe(goal_obs, 0, 0u, 0, brush);
-  fw.blank();
-  fw.forward_rand(rand ? rand + (size_t)len * 3 * C : nullptr, r0, r1, e, ep, kRandStart);
-  fw.paint(fw.s.elem_ids[elem], x * grid, y * grid, brush);
+  fw.forward_rand(rand ? rand + (size_t)q * 3 * C : nullptr, r0, r1, e, ep, slot);
+  fw.paint(fw.s.elem_ids[pe], px * grid, py * grid, brush);
 }
 
 template <int WS>
-__global__ void __launch_bounds__(256) pwf_reset_kernel(const PowderParams* __restrict__ Pp, PowderState S,
+__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(OGBX_PWF_WAVES))) pwf_reset_kernel(const PowderParams* __restrict__ Pp, PowderState S,
                                                         const int32_t* __restrict__ task_id,
                                                         const uint8_t* __restrict__ mask,
                                                         const int32_t* __restrict__ reset_action,
@@ -574,7 +587,7 @@ __global__ void __launch_bounds__(256) pwf_reset_kernel(const PowderParams* __re
   __shared__ PwFullShared<WS> sh;
   const int64_t e = blockIdx.x;
   if (mask != nullptr && mask[e] == 0) return;
-  FullWorld<WS> fw(sh);
+  FW<WS> fw(sh);
   pwf_tables(sh, Pp);
   const int ne = Pp->num_elems, xy = Pp->xy_size, nt = Pp->num_tasks;
   const uint32_t ep = S.episode[e] + 1u;
@@ -588,10 +601,12 @@ __global__ void __launch_bounds__(256) pwf_reset_kernel(const PowderParams* __re
     x = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
     y = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
   }
-  pwf_reset_env(fw, Pp, task, elem, x, y, rand ? rand + (size_t)e * rand_rows * 3 * C : nullptr, r0, r1, e, ep,
-                goal_obs + (size_t)e * C * 6);
+  const int len = Pp->seq_len[task - 1];
+  for (int q = 0; q <= len; ++q)
+    pwf_reset_op(fw, Pp, task, q, elem, x, y, rand ? rand + (size_t)e * rand_rows * 3 * C : nullptr, r0, r1, e, ep,
+                 goal_obs + (size_t)e * C * 6);
 #pragma unroll
-  for (int k = 0; k < FullWorld<WS>::CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
+  for (int k = 0; k < FW<WS>::CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
   fw.store(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
   const int errs = fw.errors();
   fw.observe(obs + (size_t)e * C * 6, 0, 0u, 0, Pp->brush);
@@ -605,15 +620,15 @@ __global__ void __launch_bounds__(256) pwf_reset_kernel(const PowderParams* __re
 // k_steps env steps; rand: [k, N, 3, H, W] injected fields for the forward of
 // each third step, or NULL = Philox (auto-resets always use Philox).
 template <int WS>
-__global__ void __launch_bounds__(256) pwf_step_kernel(
+__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(OGBX_PWF_WAVES))) pwf_step_kernel(
     const PowderParams* __restrict__ Pp, PowderState S, int64_t n, const int32_t* __restrict__ action,
     const int32_t* __restrict__ draws, const float* __restrict__ rand, int32_t k_steps, uint8_t* __restrict__ obs,
     float* __restrict__ reward, uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated,
     uint8_t* __restrict__ success, int32_t auto_reset, uint32_t k0, uint32_t k1, uint32_t a0, uint32_t a1,
     uint32_t r0, uint32_t r1) {
-  constexpr int C = WS * WS, CPT = FullWorld<WS>::CPT;
+  constexpr int C = WS * WS, CPT = FW<WS>::CPT;
   __shared__ PwFullShared<WS> sh;
-  FullWorld<WS> fw(sh);
+  FW<WS> fw(sh);
   const int64_t e = blockIdx.x;
   pwf_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
@@ -628,10 +643,11 @@ __global__ void __launch_bounds__(256) pwf_step_kernel(
   const int tol = Pp->tol_task[(task >= 1 && task <= Pp->num_tasks ? task : 1) - 1];
   bool dirty = false, goal_dirty = false;
   __syncthreads();
+  const int len = Pp->seq_len[task - 1];
   for (int k = 0; k < k_steps; ++k) {
     const int64_t o = (int64_t)k * n + e;
     const int act = action[o];
-    int stage = ctrl & 3, elem = (ctrl >> 2) & 63, x = (ctrl >> 8) & 255;
+    int stage = ctrl & 3, elem = (ctrl >> 2) & 63, x = (ctrl >> 8) & 255, y = 0;
     bool succ = (ctrl & kCtrlSuccess) != 0;
     auto rnd = [&](int bound) -> int {
       if (draws) return draws[o];
@@ -642,27 +658,47 @@ __global__ void __launch_bounds__(256) pwf_step_kernel(
     } else if (stage == 1) {
       x = act >= 0 && act < xy ? act : rnd(xy);
     } else {
-      const int y = act >= 0 && act < xy ? act : rnd(xy);
-      fw.forward_rand(rand ? rand + (size_t)o * 3 * C : nullptr, r0, r1, e, ep, kRandStep | (uint32_t)el);
-      fw.paint(sh.elem_ids[elem], x * grid, y * grid, brush);
-      succ = fw.errors() < tol;
-      dirty = true;
+      y = act >= 0 && act < xy ? act : rnd(xy);
     }
+    const bool fw_step = stage == 2;
+    const uint32_t el_step = (uint32_t)el;
     stage = stage == 2 ? 0 : stage + 1;
     el += 1;
     const bool trunc = el >= max_steps;
-    if (threadIdx.x == 0) {
-      reward[o] = succ ? 1.0f : 0.0f;
-      terminated[o] = succ;
-      truncated[o] = trunc;
-      success[o] = succ;
+    // ops: -1 = this step's forward + paint, 0..len = an auto-reset (one loop,
+    // one inlined forward)
+    int op = fw_step ? -1 : 0, op_end = fw_step ? -1 : -2;
+    int re = 0, rx = 0, ry = 0;
+    bool reset = false;
+    auto finish_step = [&]() {
+      if (threadIdx.x == 0) {
+        reward[o] = succ ? 1.0f : 0.0f;
+        terminated[o] = succ;
+        truncated[o] = trunc;
+        success[o] = succ;
+      }
+      if (auto_reset && (succ || trunc)) {
+        reset = true;
+        ep += 1u;
+        re = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
+        rx = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
+        ry = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+        op_end = len;
+      }
+    };
+    if (!fw_step) finish_step();
+    for (; op <= op_end; ++op) {
+      if (op < 0) {
+        fw.forward_rand(rand ? rand + (size_t)o * 3 * C : nullptr, r0, r1, e, ep, kRandStep | el_step);
+        fw.paint(sh.elem_ids[elem], x * grid, y * grid, brush);
+        succ = fw.errors() < tol;
+        dirty = true;
+        finish_step();
+      } else {
+        pwf_reset_op(fw, Pp, task, op, re, rx, ry, nullptr, r0, r1, e, ep, nullptr);
+      }
     }
-    if (auto_reset && (succ || trunc)) {
-      ep += 1u;
-      const int re = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
-      const int rx = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
-      const int ry = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
-      pwf_reset_env(fw, Pp, task, re, rx, ry, nullptr, r0, r1, e, ep, nullptr);
+    if (reset) {
       succ = fw.errors() < tol;
       stage = 0;
       el = 0;
@@ -688,13 +724,13 @@ __global__ void __launch_bounds__(256) pwf_step_kernel(
 // float32 layout (tests / drop-in): rand [steps, n, 3, H, W] or NULL (Philox
 // keyed by the env seed); optional render of the result (n, H, W, 3).
 template <int WS>
-__global__ void __launch_bounds__(256) pwf_forward_kernel(const PowderParams* __restrict__ Pp,
+__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(OGBX_PWF_WAVES))) pwf_forward_kernel(const PowderParams* __restrict__ Pp,
                                                           const float* __restrict__ in, int64_t n, int32_t steps,
                                                           const float* __restrict__ rand, float* __restrict__ out,
                                                           uint8_t* __restrict__ rgb, uint32_t r0, uint32_t r1) {
-  constexpr int C = WS * WS, CPT = FullWorld<WS>::CPT;
+  constexpr int C = WS * WS, CPT = FW<WS>::CPT;
   __shared__ PwFullShared<WS> sh;
-  FullWorld<WS> fw(sh);
+  FW<WS> fw(sh);
   const int64_t e = blockIdx.x;
   pwf_tables(sh, Pp);
   const float* w = in + (size_t)e * 9 * C;
@@ -858,6 +894,13 @@ using namespace ogbx;
 
 namespace {
 // dispatch a kernel template on the world size
+#define PWF_LAUNCH(kern, e, grid, stream, ...)                                                 \
+  do {                                                                                         \
+    if ((e)->P.W == 64)                                                                        \
+      hipLaunchKernelGGL(kern<64>, dim3(grid), dim3(pwf_nt<64>()), 0, (hipStream_t)(stream), __VA_ARGS__); \
+    else                                                                                       \
+      hipLaunchKernelGGL(kern<32>, dim3(grid), dim3(pwf_nt<32>()), 0, (hipStream_t)(stream), __VA_ARGS__); \
+  } while (0)
 #define PW_LAUNCH(kern, e, grid, stream, ...)                                                  \
   do {                                                                                         \
     if ((e)->P.W == 64)                                                                        \
@@ -1024,7 +1067,7 @@ ogbx_status ogbx_powder_reset(ogbx_powder_t e, const int32_t* task_id, const uin
   seed_key(seed, kTagPowderReset, &k0, &k1);
   seed_key(seed, kTagPowderRand, &r0, &r1);
   if (e->full) {
-    PW_LAUNCH(pwf_reset_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, task_id, mask, reset_action, rand,
+    PWF_LAUNCH(pwf_reset_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, task_id, mask, reset_action, rand,
               rand_rows, obs, goal_obs, k0, k1, r0, r1);
     OGBX_LAUNCHED("pwf_reset_kernel");
   } else {
@@ -1051,7 +1094,7 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
   seed_key(e->seed, kTagPowderAction, &a0, &a1);
   seed_key(e->seed, kTagPowderRand, &r0, &r1);
   if (e->full) {
-    PW_LAUNCH(pwf_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps, obs,
+    PWF_LAUNCH(pwf_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps, obs,
               reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1, r0, r1);
     OGBX_LAUNCHED("pwf_step_kernel");
   } else {
@@ -1102,7 +1145,7 @@ ogbx_status ogbx_powder_forward_full(ogbx_powder_t e, const float* world_in, int
   OGBX_HIP(hipSetDevice(e->device));
   uint32_t r0, r1;
   seed_key(e->seed, kTagPowderRand, &r0, &r1);
-  PW_LAUNCH(pwf_forward_kernel, e, (uint32_t)n_worlds, stream, e->Pd, world_in, n_worlds, steps, rand, world_out,
+  PWF_LAUNCH(pwf_forward_kernel, e, (uint32_t)n_worlds, stream, e->Pd, world_in, n_worlds, steps, rand, world_out,
             rgb_out, r0, r1);
   OGBX_LAUNCHED("pwf_forward_kernel");
   return OGBX_OK;

@@ -27,21 +27,34 @@ enum PwElem : int {
   kLemming = 18
 };
 
+// LDS of one env: 116 KB at 64x64 (one 1024-thread workgroup per CU), 29 KB
+// at 32x32.  Every rule writes its result to the staging copy (a2, m2, v2 or
+// the scratch flags) and the owners copy it back after a barrier, so no
+// per-thread arrays are needed: loops over a thread's cells stay rolled and
+// the register footprint small.
 template <int WS>
 struct alignas(16) PwFullShared {
   static constexpr int C = WS * WS;
   alignas(16) uint8_t a[C];
   alignas(16) int8_t m[C];
   alignas(16) float2 v[C];
-  alignas(16) uint8_t f1[C];
-  alignas(16) uint8_t f2[C];
-  alignas(16) int16_t cnt[C];
-  alignas(16) int8_t sw[C];
-  alignas(16) uint8_t g[C];              // this env's goal ids
-  alignas(16) uint32_t ob[C * 6 / 4];    // observation staging
+  alignas(16) uint8_t g[C];    // this env's goal ids
+  alignas(16) uint16_t rb[C];  // rand decision bits of the current forward (rand_bits)
+  alignas(16) uint8_t a2[C];   // staging copy of the state (moves)
+  alignas(16) int8_t m2[C];
+  alignas(16) float2 v2[C];
+  union {
+    struct {  // rule scratch
+      alignas(16) uint8_t f1[C];
+      alignas(16) uint8_t f2[C];
+      alignas(16) int16_t cnt[C];
+      alignas(16) int8_t sw[C];
+    };
+    alignas(16) uint32_t ob[C * 6 / 4];  // observation staging (between forwards)
+  };
   uint32_t lut[32];
   int32_t elem_ids[8];
-  int32_t red[4];
+  int32_t red[16];
 };
 
 // render colours as float32 c / 255 (sim.py:402-453), velocity colour
@@ -67,27 +80,34 @@ __device__ __forceinline__ uint32_t fgrav(uint32_t a) { return (a >> 5) & 1u; }
 __device__ __forceinline__ uint32_t fdidg(uint32_t a) { return (a >> 6) & 1u; }
 __device__ __forceinline__ float fdens(uint32_t a) { return (float)((kDensPacked >> (3u * (a & 31u))) & 7u); }
 
-// Workgroup-level full forward on the LDS state of one world.  Thread t owns
-// CPT consecutive cells of one row.  rm/ri/re: this thread's rand values.
-template <int WS>
-struct FullWorld {
-  static constexpr int H = WS, W = WS, C = WS * WS, CPT = C / 256, TPR = W / CPT;
-  PwFullShared<WS>& s;
-  int r, c0;
-  __device__ __forceinline__ explicit FullWorld(PwFullShared<WS>& sh)
-      : s(sh), r((int)threadIdx.x / TPR), c0(((int)threadIdx.x % TPR) * CPT) {}
+constexpr uint32_t bit(int id) { return 1u << id; }
+constexpr uint32_t kVelBit = 1u << 31;  // presence mask: some velocity is nonzero
 
-  __device__ __forceinline__ int cell(int k) const { return r * W + c0 + k; }
+// Workgroup-level full forward on the LDS state of one world, NT threads.
+// Thread t owns the CPT cells of column t % W in rows t / W + k * (NT / W):
+// for every k the workgroup touches NT consecutive cells, so byte arrays are
+// conflict-free and float2 velocities take the natural two LDS passes.
+template <int WS, int NT>
+struct FullWorld {
+  static constexpr int H = WS, W = WS, C = WS * WS, CPT = C / NT, RPK = NT / W;
+  static_assert(NT % W == 0 && CPT * RPK == H, "whole rows per slab");
+  PwFullShared<WS>& s;
+  int r0, col;
+  __device__ __forceinline__ explicit FullWorld(PwFullShared<WS>& sh)
+      : s(sh), r0((int)threadIdx.x / W), col((int)threadIdx.x % W) {}
+
+  __device__ __forceinline__ int row(int k) const { return r0 + k * RPK; }
+  __device__ __forceinline__ int cell(int k) const { return row(k) * W + col; }
   // periodic neighbour (np.roll semantics)
   __device__ __forceinline__ int nb(int k, int dr, int dc) const {
-    int rr = r + dr, cc = c0 + k + dc;
+    int rr = row(k) + dr, cc = col + dc;
     rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
     cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
     return rr * W + cc;
   }
   // zero-padded neighbour (conv2d padding=1): -1 outside
   __device__ __forceinline__ int zp(int k, int dr, int dc) const {
-    const int rr = r + dr, cc = c0 + k + dc;
+    const int rr = row(k) + dr, cc = col + dc;
     return (rr < 0 || rr >= H || cc < 0 || cc >= W) ? -1 : rr * W + cc;
   }
   __device__ __forceinline__ void sync() const { __syncthreads(); }
@@ -109,20 +129,47 @@ struct FullWorld {
   template <typename P>
   __device__ __forceinline__ int box(int k, P pred) const {
     int n = 0;
-#pragma unroll
-    for (int dr = -1; dr <= 1; ++dr)
-#pragma unroll
-      for (int dc = -1; dc <= 1; ++dc) {
-        const int j = zp(k, dr, dc);
-        n += (j >= 0 && pred(fid(s.a[j]))) ? 1 : 0;
-      }
+#pragma unroll 1
+    for (int q = 0; q < 9; ++q) {  // rolled: keeps the register footprint small
+      const int j = zp(k, q / 3 - 1, q % 3 - 1);
+      n += (j >= 0 && pred(fid(s.a[j]))) ? 1 : 0;
+    }
     return n;
   }
 
   // ------------------------------------------------------------- rules
-  __device__ void stone() const {
-    uint8_t na[CPT];
-#pragma unroll
+  // Staged writes: stage(i, ...) into the copy, commit() copies own cells back.
+  __device__ __forceinline__ void stage(int i, uint32_t a, int m, float2 v) const {
+    s.a2[i] = (uint8_t)a;
+    s.m2[i] = (int8_t)m;
+    s.v2[i] = v;
+  }
+  __device__ __forceinline__ void stage_from(int i, int j) const { stage(i, s.a[j], s.m[j], s.v[j]); }
+  __device__ __forceinline__ void commit() const {
+    sync();
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) {
+      const int i = cell(k);
+      s.a[i] = s.a2[i];
+      s.m[i] = s.m2[i];
+      s.v[i] = s.v2[i];
+    }
+    sync();
+  }
+  // element conversions: f1[i] = new id + 1 (0 = unchanged) -> own cells
+  __device__ __forceinline__ void commit_conversions() const {
+    sync();
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) {
+      const int i = cell(k);
+      const uint32_t to = s.f1[i];
+      if (to) put(i, elem(to - 1));
+    }
+    sync();
+  }
+
+  __device__ __forceinline__ void stone() const {
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       uint32_t a = s.a[i];
@@ -131,73 +178,56 @@ struct FullWorld {
         const int sup = (jl >= 0 && fid(s.a[jl]) == kStone) + (jr >= 0 && fid(s.a[jr]) == kStone);
         a = (a & ~kGrav) | (sup < 2 ? kGrav : 0u);
       }
-      na[k] = (uint8_t)a;
+      s.a2[i] = (uint8_t)a;
     }
     sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) s.a[cell(k)] = na[k];
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) s.a[cell(k)] = s.a2[cell(k)];
     sync();
   }
 
-  __device__ void gravity() const {
-    // did-gravity reset where gravity == 1 (own cells), then the move flags
-#pragma unroll
+  // BehaviorGravity (sim.py:461-501).  The did-gravity reset (rd) is applied
+  // to every staged value; moves are decided locally from rows r-2..r+1
+  // (real = dbb & ~dbb(above), real_up = real(above)), no flag pass.
+  __device__ static __forceinline__ uint32_t rd(uint32_t a) { return fgrav(a) ? (a & ~kDidg) : a; }
+  __device__ __forceinline__ bool dbb(int i, int ib) const {
+    const uint32_t a = s.a[i], b = s.a[ib];
+    return (fdens(b) - fdens(a) < 0.0f) && fgrav(a) && fgrav(b);
+  }
+  __device__ __forceinline__ void gravity() const {
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const uint32_t a = s.a[i];
-      if (fgrav(a)) s.a[i] = (uint8_t)(a & ~kDidg);
-    }
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const uint32_t a = s.a[cell(k)], b = s.a[nb(k, 1, 0)];
-      s.f1[cell(k)] = (fdens(b) - fdens(a) < 0.0f) && fgrav(a) && fgrav(b);
-    }
-    sync();
-    Cell nc[CPT];
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const bool real = s.f1[i] && !s.f1[nb(k, -1, 0)];
-      const bool real_up = s.f1[nb(k, -1, 0)] && !s.f1[nb(k, -2, 0)];
-      if (real) {
-        nc[k] = get(nb(k, 1, 0));
-      } else if (real_up) {
-        nc[k] = get(nb(k, -1, 0));
-        nc[k].a |= (uint8_t)kDidg;
+      const int i = cell(k), up = nb(k, -1, 0), up2 = nb(k, -2, 0), dn = nb(k, 1, 0);
+      const bool d0 = dbb(i, dn), d1 = dbb(up, i), d2 = dbb(up2, up);
+      if (d0 && !d1) {
+        stage(i, rd(s.a[dn]), s.m[dn], s.v[dn]);
+      } else if (d1 && !d2) {
+        stage(i, rd(s.a[up]) | kDidg, s.m[up], s.v[up]);
       } else {
-        nc[k] = get(i);
+        stage(i, rd(s.a[i]), s.m[i], s.v[i]);
       }
     }
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) put(cell(k), nc[k]);
-    sync();
+    commit();
   }
 
-  __device__ void sand(const float* rm) const {
-#pragma unroll
+  __device__ __forceinline__ void sand() const {
+#pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
-      const int go = pass == 0 ? -1 : 1;  // fall toward -1 (left) then +1 (right)
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) s.f2[cell(k)] = pass == 0 ? (rm[k] > 0.5f) : (rm[k] <= 0.5f);
-      sync();
-      Cell nc[CPT];
-#pragma unroll
+      const int go = pass == 0 ? -1 : 1;        // fall toward -1 (left) then +1 (right)
+      const uint32_t fl = pass == 0 ? 1u : 0u;  // fall_dir: rm > 0.5, then rm <= 0.5
+#pragma unroll 1
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), ibl = nb(k, 1, go), iar = nb(k, -1, -go);
         const uint32_t a = s.a[i], bl = s.a[ibl], ar = s.a[iar];
         const bool elem = fid(a) == kSand || fid(a) == kDust;
         const bool elem_ar = fid(ar) == kSand || fid(ar) == kDust;
         const bool ndg = !fdidg(a);
-        const bool mv = elem && !fdidg(bl) && s.f2[i] && (fdens(a) - fdens(bl) > 0.0f) && fgrav(bl) && ndg;
-        const bool in = elem_ar && !fdidg(ar) && s.f2[iar] && (fdens(ar) - fdens(a) > 0.0f) && fgrav(ar) && ndg;
-        nc[k] = mv ? get(ibl) : (in ? get(iar) : get(i));
+        const bool f_own = (s.rb[i] & 1u) == fl, f_ar = (s.rb[iar] & 1u) == fl;
+        const bool mv = elem && !fdidg(bl) && f_own && (fdens(a) - fdens(bl) > 0.0f) && fgrav(bl) && ndg;
+        const bool in = elem_ar && !fdidg(ar) && f_ar && (fdens(ar) - fdens(a) > 0.0f) && fgrav(ar) && ndg;
+        stage_from(i, mv ? ibl : (in ? iar : i));
       }
-      sync();
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) put(cell(k), nc[k]);
-      sync();
+      commit();
     }
   }
 
@@ -205,77 +235,82 @@ struct FullWorld {
     return id == kEmpty || id == kWater || id == kGas || id == kLava || id == kAcid;
   }
 
-  __device__ void fluid(const float* rm) const {
-    float mom[CPT];
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) mom[k] = 0.0f;
-#pragma unroll
+  // FluidFlow (sim.py:593-667), two passes (left, then right).  A cell's move
+  // decision mv needs only its own state and its side neighbour's, so real
+  // (mv & ~mv(back)) and real_in (real(back)) are evaluated locally from three
+  // cells of the row.  New momentum per position: sw after pass 1 (0 / +2),
+  // f1 (as int8) after pass 2.
+  __device__ __forceinline__ bool fluid_mv(int j, int side, int pass, int mom) const {
+    const uint32_t a = s.a[j], sd = s.a[side];
+    const int m6 = s.m[j] < 0 ? 0 : (s.m[j] > 0 ? 2 : 1);
+    // (rm + ch6) + mom > 0.5 for ch6 in {-2, 0, 2}, mom in {0, 2}: rand_bits
+    const bool fall = (s.rb[j] >> (1 + m6 + (mom != 0 ? 3 : 0))) & 1u;
+    const bool match = pass == 0 ? fall : !fall;
+    const bool air = fid(a) == kKangaroo || fid(a) == kLemming;
+    const bool elem = is_fluid(fid(a)) || air;
+    return match && elem && (!fdidg(a) || air) && (fdens(a) - fdens(sd) > 0.0f) && fgrav(sd) && fgrav(a);
+  }
+  __device__ __forceinline__ void fluid() const {
+    int8_t* mom2 = reinterpret_cast<int8_t*>(s.f1);
+#pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       const int go = pass == 0 ? -1 : 1;
-#pragma unroll
+#pragma unroll 1
       for (int k = 0; k < CPT; ++k) {
-        const int i = cell(k);
-        const uint32_t a = s.a[i], sd = s.a[nb(k, 0, go)];
-        const bool fall = (rm[k] + (float)s.m[i]) + mom[k] > 0.5f;
-        const bool match = pass == 0 ? fall : !fall;
-        const bool air = fid(a) == kKangaroo || fid(a) == kLemming;
-        const bool elem = is_fluid(fid(a)) || air;
-        s.f1[i] = match && elem && (!fdidg(a) || air) && (fdens(a) - fdens(sd) > 0.0f) && fgrav(sd) && fgrav(a);
+        const int i = cell(k), sd = nb(k, 0, go), b1 = nb(k, 0, -go), b2 = nb(k, 0, -2 * go);
+        const int mom_i = pass == 0 ? 0 : s.sw[i], mom_b1 = pass == 0 ? 0 : s.sw[b1];
+        const int mom_b2 = pass == 0 ? 0 : s.sw[b2];
+        const bool mv0 = fluid_mv(i, sd, pass, mom_i), mv1 = fluid_mv(b1, i, pass, mom_b1);
+        const bool mv2 = fluid_mv(b2, b1, pass, mom_b2);
+        const bool real = mv0 && !mv1, real_in = mv1 && !mv2;
+        const int nm = mom_i + (real_in ? (pass == 0 ? 2 : -2) : 0);
+        if (pass == 0) {
+          s.f2[i] = (uint8_t)nm;  // staged: sw is read by the neighbours this pass
+        } else {
+          mom2[i] = (int8_t)nm;
+        }
+        stage_from(i, real ? sd : (real_in ? b1 : i));
       }
       sync();
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) s.f2[cell(k)] = s.f1[cell(k)] && !s.f1[nb(k, 0, -go)];
-      sync();
-      Cell nc[CPT];
-#pragma unroll
+#pragma unroll 1
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
-        const bool real = s.f2[i], real_in = s.f2[nb(k, 0, -go)];
-        if (real_in) mom[k] = mom[k] + (pass == 0 ? 2.0f : -2.0f);
-        nc[k] = real ? get(nb(k, 0, go)) : (real_in ? get(nb(k, 0, -go)) : get(i));
+        s.a[i] = s.a2[i];
+        s.m[i] = s.m2[i];
+        s.v[i] = s.v2[i];
+        if (pass == 0) s.sw[i] = (int8_t)s.f2[i];
       }
-      sync();
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) put(cell(k), nc[k]);
       sync();
     }
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
-      if (is_fluid(id) || id == kKangaroo || id == kLemming) s.m[i] = (int8_t)mom[k];
+      if (is_fluid(id) || id == kKangaroo || id == kLemming) s.m[i] = mom2[i];
     }
     sync();
   }
 
-  // element conversions of own cells decided from the current ids
-  template <typename Rule>
-  __device__ __forceinline__ void convert(Rule rule) const {
-    int to[CPT];
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) to[k] = rule(k);
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k)
-      if (to[k] >= 0) put(cell(k), elem((uint32_t)to[k]));
-    sync();
+  __device__ __forceinline__ void ice() const {
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) {
+      const uint32_t id = fid(s.a[cell(k)]);
+      bool to = id == kIce && ri_lt(k, kRi002);
+      if (to) to = box(k, [](uint32_t x) { return x == kEmpty || x == kFire || x == kLava || x == kWater; }) > 1;
+      s.f1[cell(k)] = to ? kWater + 1 : 0;
+    }
+    commit_conversions();
   }
 
-  __device__ void ice(const float* ri) const {
-    convert([&](int k) {
+  __device__ __forceinline__ void water() const {
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
-      if (id != kIce || !(ri[k] < 0.02f)) return -1;
-      const int n = box(k, [](uint32_t x) { return x == kEmpty || x == kFire || x == kLava || x == kWater; });
-      return n > 1 ? (int)kWater : -1;
-    });
-  }
-
-  __device__ void water(const float* re) const {
-    convert([&](int k) {
-      const uint32_t id = fid(s.a[cell(k)]);
-      if (id != kWater || !(re[k] < 0.05f)) return -1;
-      return box(k, [](uint32_t x) { return x == kIce; }) >= 3 ? (int)kIce : -1;
-    });
+      bool to = id == kWater && re_lt(k, kRe005);
+      if (to) to = box(k, [](uint32_t x) { return x == kIce; }) >= 3;
+      s.f1[cell(k)] = to ? kIce + 1 : 0;
+    }
+    commit_conversions();
   }
 
   __device__ static __forceinline__ bool burnable(uint32_t x) {
@@ -283,92 +318,107 @@ struct FullWorld {
            x == kMole || x == kLemming;
   }
 
-  __device__ void fire(const float* ri, const float* re) const {
-    bool fl[CPT];
-    int conv_to[CPT];
-#pragma unroll
+  __device__ __forceinline__ void fire() const {
+    // f1 bit 0: burns (pushes its 4 neighbours with 8), bit 1: dust near fire
+    // (pushes with 30), bit 2: fire or lava before the burn; f2: conversion
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
-      fl[k] = id == kFire || id == kLava;
+      const bool fl = id == kFire || id == kLava;
       const bool near = box(k, [](uint32_t x) { return x == kFire || x == kLava; }) > 0;
-      const float p = ri[k];
-      const bool burn = ((id == kWood && p < 0.05f) || (id == kPlant && p < 0.2f) || (id == kGas && p < 0.2f) ||
-                         id == kDust || (id == kBird && p < 0.05f) ||
-                         ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p < 0.2f)) &&
+      const bool p005 = ri_lt(k, kRi005), p02 = ri_lt(k, kRi02);
+      const bool burn = ((id == kWood && p005) || (id == kPlant && p02) || (id == kGas && p02) || id == kDust ||
+                         (id == kBird && p005) ||
+                         ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p02)) &&
                         near;
-      const bool burn_ice = id == kIce && p < 0.2f && near;
-      s.f1[i] = burn;                   // pushes its 4 neighbours with 8
-      s.f2[i] = id == kDust && near;    // and dust with 30
-      conv_to[k] = burn ? (int)kFire : (burn_ice ? (int)kWater : -1);
+      const bool burn_ice = id == kIce && p02 && near;
+      s.f1[i] = (uint8_t)((burn ? 1 : 0) | (id == kDust && near ? 2 : 0) | (fl ? 4 : 0));
+      s.f2[i] = burn ? kFire + 1 : (burn_ice ? kWater + 1 : 0);
     }
     sync();
-    float2 nv[CPT];
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
-      float2 v = s.v[cell(k)];
+      const int i = cell(k);
+      float2 v = s.v[i];
       // impulses away from a burning neighbour (sim.py:744-752): left, above, below, right
-      v.y = v.y + 8.0f * (float)s.f1[nb(k, 0, -1)];
-      v.x = v.x + 8.0f * (float)s.f1[nb(k, -1, 0)];
-      v.x = v.x - 8.0f * (float)s.f1[nb(k, 1, 0)];
-      v.y = v.y - 8.0f * (float)s.f1[nb(k, 0, 1)];
-      v.y = v.y + 30.0f * (float)s.f2[nb(k, 0, -1)];
-      v.x = v.x + 30.0f * (float)s.f2[nb(k, -1, 0)];
-      v.x = v.x - 30.0f * (float)s.f2[nb(k, 1, 0)];
-      v.y = v.y - 30.0f * (float)s.f2[nb(k, 0, 1)];
-      nv[k] = v;
+      const uint32_t L = s.f1[nb(k, 0, -1)], U = s.f1[nb(k, -1, 0)], D = s.f1[nb(k, 1, 0)], R = s.f1[nb(k, 0, 1)];
+      v.y = v.y + 8.0f * (float)(L & 1);
+      v.x = v.x + 8.0f * (float)(U & 1);
+      v.x = v.x - 8.0f * (float)(D & 1);
+      v.y = v.y - 8.0f * (float)(R & 1);
+      v.y = v.y + 30.0f * (float)((L >> 1) & 1);
+      v.x = v.x + 30.0f * (float)((U >> 1) & 1);
+      v.x = v.x - 30.0f * (float)((D >> 1) & 1);
+      v.y = v.y - 30.0f * (float)((R >> 1) & 1);
+      s.v2[i] = v;
     }
     sync();
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
-      s.v[cell(k)] = nv[k];
-      if (conv_to[k] >= 0) put(cell(k), elem((uint32_t)conv_to[k]));
+      const int i = cell(k);
+      const uint32_t to = s.f2[i];
+      if (to) {
+        put(i, elem(to - 1));
+      } else {
+        s.v[i] = s.v2[i];
+      }
     }
     sync();
     // fire spread from (fire or lava before the burn) x burnable neighbours, and lava
-    int nbr[CPT];
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
-      nbr[k] = box(k, [](uint32_t x) { return burnable(x); });
-      s.cnt[cell(k)] = (int16_t)(nbr[k] * (fl[k] ? 1 : 0) + (fid(s.a[cell(k)]) == kLava ? 1 : 0));
+      const int i = cell(k);
+      const int nbr = box(k, [](uint32_t x) { return burnable(x); });
+      s.cnt[i] = (int16_t)(nbr * ((s.f1[i] >> 2) & 1) + (fid(s.a[i]) == kLava ? 1 : 0));
+      s.f2[i] = (uint8_t)(nbr == 0);
     }
     sync();
-    int to[CPT];
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
-      int in_range = 0;
-#pragma unroll
-      for (int dr = -1; dr <= 1; ++dr)
-#pragma unroll
-        for (int dc = -1; dc <= 1; ++dc) {
-          const int j = zp(k, dr, dc);
+      const int i = cell(k);
+      const uint32_t id = fid(s.a[i]);
+      bool burn_empty = false;
+      if (id == kEmpty && ri_lt(k, kRi03)) {
+        int in_range = 0;
+#pragma unroll 1
+        for (int q = 0; q < 9; ++q) {
+          const int j = zp(k, q / 3 - 1, q % 3 - 1);
           in_range += j >= 0 ? s.cnt[j] : 0;
         }
-      const uint32_t id = fid(s.a[cell(k)]);
-      const bool burn_empty = id == kEmpty && in_range > 0 && ri[k] < 0.3f;
+        burn_empty = in_range > 0;
+      }
       const uint32_t id2 = burn_empty ? (uint32_t)kFire : id;
-      const bool fade = id2 == kFire && re[k] < 0.4f && nbr[k] == 0;
-      to[k] = fade ? (int)kEmpty : (burn_empty ? (int)kFire : -1);
+      const bool fade = id2 == kFire && re_lt(k, kRe04) && s.f2[i];
+      s.sw[i] = (int8_t)(fade ? kEmpty + 1 : (burn_empty ? kFire + 1 : 0));
     }
     sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k)
-      if (to[k] >= 0) put(cell(k), elem((uint32_t)to[k]));
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) {
+      const int i = cell(k);
+      const int to = s.sw[i];
+      if (to) put(i, elem((uint32_t)(to - 1)));
+    }
     sync();
   }
 
-  __device__ void plant(const float* ri) const {
-    convert([&](int k) {
+  __device__ __forceinline__ void plant() const {
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
-      if (id != kWater && id != kEmpty) return -1;
-      const int cnt = box(k, [](uint32_t x) { return x == kPlant; });
-      const bool grow = id == kWater && ri[k] < 0.05f;
-      bool to_plant = grow && cnt <= 3 && cnt >= 1;
-      const bool to_empty = grow && cnt > 3;
-      if (!to_plant && id == kEmpty && ri[k] < 0.2f && cnt > 0)
-        to_plant = box(k, [](uint32_t x) { return x == kIce || x == kWood; }) > 0;
-      return to_plant ? (int)kPlant : (to_empty ? (int)kEmpty : -1);
-    });
+      int to = 0;
+      if (id == kWater || id == kEmpty) {
+        const int cnt = box(k, [](uint32_t x) { return x == kPlant; });
+        const bool grow = id == kWater && ri_lt(k, kRi005);
+        bool to_plant = grow && cnt <= 3 && cnt >= 1;
+        const bool to_empty = grow && cnt > 3;
+        if (!to_plant && id == kEmpty && ri_lt(k, kRi02) && cnt > 0)
+          to_plant = box(k, [](uint32_t x) { return x == kIce || x == kWood; }) > 0;
+        to = to_plant ? kPlant + 1 : (to_empty ? kEmpty + 1 : 0);
+      }
+      s.f1[cell(k)] = (uint8_t)to;
+    }
+    commit_conversions();
   }
 
   // direction d (sim.py direction_func) as (dr, dc): 0 right, 1 below-right,
@@ -378,53 +428,78 @@ struct FullWorld {
     dc = (int)((0x901Au >> (2 * d)) & 3u) - 1;
   }
 
-  __device__ void velocity() const {
+  __device__ __forceinline__ void velocity() const {
     const float inv2pi = (float)(1.0 / (2.0 * 3.141592653589793));
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
-      int bin[CPT];
-      bool enough[CPT];
-#pragma unroll
+      // f2 = angle bin of cells that may move (mag above the pass threshold, not
+      // wall), 0xFF otherwise; sw = chosen swap direction (-1 none)
+      uint32_t dirs = 0;  // angle bins present among the cells that may move
+#pragma unroll 1
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
         const float2 v = s.v[i];
         const float mag = sqrtf(v.x * v.x + v.y * v.y);
-        const float q = v.y / (mag + 0.001f);
-        const float raw = inv2pi * (float)acos((double)q);
-        const float ang = v.x < 0.0f ? 1.0f - raw : raw;
-        float b = floorf(ang * 8.0f + 0.5f);
-        b = b - 8.0f * floorf(b / 8.0f);  // np.remainder(., 8) for b >= 0
-        bin[k] = (int)b;
-        enough[k] = mag > (pass == 0 ? 1.0f : 2.0f) && fid(s.a[i]) != kWall;
+        uint8_t b8 = 0xFF;
+        if (mag > (pass == 0 ? 1.0f : 2.0f) && fid(s.a[i]) != kWall) {
+          const float q = v.y / (mag + 0.001f);
+          const float raw = inv2pi * (float)acos((double)q);
+          const float ang = v.x < 0.0f ? 1.0f - raw : raw;
+          float b = floorf(ang * 8.0f + 0.5f);
+          b = b - 8.0f * floorf(b / 8.0f);  // np.remainder(., 8) for b >= 0
+          b8 = (uint8_t)(int)b;
+          dirs |= 1u << b8;
+        }
+        s.f2[i] = b8;
         s.sw[i] = -1;
       }
-      sync();
+      dirs = block_or(dirs);
+      if (dirs == 0) {
+        // no swap anywhere: v = v * 0.5 + v * 0.5 in place
+#pragma unroll 1
+        for (int k = 0; k < CPT; ++k) {
+          float2 v = s.v[cell(k)];
+          v.x = v.x * 0.5f + v.x * 0.5f;
+          v.y = v.y * 0.5f + v.y * 0.5f;
+          s.v[cell(k)] = v;
+        }
+        sync();
+        continue;
+      }
+      // swap rounds in direction order; rounds with no candidate are
+      // identities and skipped; swap choices ping-pong between sw and m2
+      int8_t* cur = s.sw;
+      int8_t* nxt = s.m2;
 #pragma unroll 1
       for (int d = 0; d < 8; ++d) {
+        if (!((dirs >> d) & 1u)) continue;
         int dr, dc;
         dir_of(d, dr, dc);
-#pragma unroll
+#pragma unroll 1
         for (int k = 0; k < CPT; ++k) {
           const int i = cell(k), j = nb(k, dr, dc);
-          s.f1[i] = bin[k] == d && enough[k] && s.sw[i] == -1 && s.sw[j] == -1 && fid(s.a[j]) == kEmpty;
+          s.f1[i] = s.f2[i] == d && cur[i] == -1 && cur[j] == -1 && fid(s.a[j]) == kEmpty;
         }
         sync();
-        int8_t nsw[CPT];
-#pragma unroll
+#pragma unroll 1
         for (int k = 0; k < CPT; ++k) {
           const int i = cell(k);
-          int8_t w = s.sw[i];
+          int8_t w = cur[i];
           if (s.f1[i]) w = (int8_t)d;
           if (s.f1[nb(k, -dr, -dc)]) w = (int8_t)((d + 4) & 7);
-          nsw[k] = w;
+          nxt[i] = w;
         }
         sync();
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) s.sw[cell(k)] = nsw[k];
+        int8_t* t = cur;
+        cur = nxt;
+        nxt = t;
+      }
+      if (cur != s.sw) {
+#pragma unroll 1
+        for (int k = 0; k < CPT; ++k) s.sw[cell(k)] = cur[cell(k)];
         sync();
       }
-      Cell nc[CPT];
-#pragma unroll
+#pragma unroll 1
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
         const int w = s.sw[i];
@@ -434,18 +509,13 @@ struct FullWorld {
           dir_of(w, dr, dc);
           j = nb(k, dr, dc);
         }
-        nc[k] = get(j);
-        const float2 old = s.v[i];
-        nc[k].v.x = nc[k].v.x * 0.5f + old.x * 0.5f;
-        nc[k].v.y = nc[k].v.y * 0.5f + old.y * 0.5f;
+        const float2 old = s.v[i], nv = s.v[j];
+        stage(i, s.a[j], s.m[j], make_float2(nv.x * 0.5f + old.x * 0.5f, nv.y * 0.5f + old.y * 0.5f));
       }
-      sync();
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) put(cell(k), nc[k]);
-      sync();
+      commit();
     }
     // decay and 3x3 blur (zero padded), NumPy's einsum summation order
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       float2 v = s.v[i];
@@ -455,8 +525,7 @@ struct FullWorld {
     }
     sync();
     const float w18 = 1.0f / 18.0f;
-    float2 nv[CPT];
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       float tx[9], ty[9];
 #pragma unroll
@@ -469,55 +538,82 @@ struct FullWorld {
       const float2 own = s.v[cell(k)];
       const float bx = (((tx[4] + tx[0]) + tx[8]) + (tx[5] + tx[1])) + ((tx[6] + tx[2]) + (tx[7] + tx[3]));
       const float by = (((ty[4] + ty[0]) + ty[8]) + (ty[5] + ty[1])) + ((ty[6] + ty[2]) + (ty[7] + ty[3]));
-      nv[k] = make_float2(bx + own.x * 0.5f, by + own.y * 0.5f);
+      s.v2[cell(k)] = make_float2(bx + own.x * 0.5f, by + own.y * 0.5f);
     }
     sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) s.v[cell(k)] = nv[k];
+#pragma unroll 1
+    for (int k = 0; k < CPT; ++k) s.v[cell(k)] = s.v2[cell(k)];
     sync();
   }
 
   // ------------------------------------------------------------- env helpers
   // Blank world: walls on the border, empty inside (powderworld_env.py:309-313).
-  __device__ void blank() const {
+  __device__ __forceinline__ void blank() const {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int c = c0 + k;
+      const int r = row(k), c = col;
       const bool border = r == 0 || r == H - 1 || c == 0 || c == W - 1;
       put(cell(k), elem(border ? (uint32_t)kWall : (uint32_t)kEmpty));
     }
     sync();
   }
 
-  // The three rand fields of one forward for this thread's cells: injected
-  // (src = [3, H, W] float32) or Philox (one 4x32 draw per cell).
-  __device__ void rands(const float* __restrict__ src, uint32_t k0, uint32_t k1, uint64_t env, uint32_t ep,
-                        uint32_t slot, float* rm, float* ri, float* re) const {
+  // Every use of a rand field in the rules is a float32 comparison with a
+  // constant after adding a few possible integers (sim.py: sand rm > 0.5;
+  // fluid (rm + ch6) + mom > 0.5 with ch6 in {-2,0,2}, mom in {0,2}; ri below
+  // 0.02/0.05/0.2/0.3; re below 0.05/0.4), so a cell's three floats reduce
+  // exactly to 12 decision bits:
+  //   bit 0 rm > 0.5 | bits 1-3 (rm + {-2,0,2}) + 0 > 0.5 | bits 4-6 ... + 2 > 0.5
+  //   | bits 7-9 ri category (0: < 0.02, 1: < 0.05, 2: < 0.2, 3: < 0.3, 4)
+  //   | bits 10-11 re category (0: < 0.05, 1: < 0.4, 2)
+  __device__ static __forceinline__ uint32_t rand_bits(float rm, float ri, float re) {
+    uint32_t b = rm > 0.5f ? 1u : 0u;
 #pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float x = rm + (float)(2 * j - 2);
+      b |= (x + 0.0f > 0.5f ? 1u : 0u) << (1 + j);
+      b |= (x + 2.0f > 0.5f ? 1u : 0u) << (4 + j);
+    }
+    const uint32_t ic = ri < 0.02f ? 0u : (ri < 0.05f ? 1u : (ri < 0.2f ? 2u : (ri < 0.3f ? 3u : 4u)));
+    const uint32_t ec = re < 0.05f ? 0u : (re < 0.4f ? 1u : 2u);
+    return b | (ic << 7) | (ec << 10);
+  }
+  static constexpr uint32_t kRi002 = 1, kRi005 = 2, kRi02 = 3, kRi03 = 4, kRe005 = 1, kRe04 = 2;
+  __device__ __forceinline__ bool ri_lt(int k, uint32_t cat) const { return ((s.rb[cell(k)] >> 7) & 7u) < cat; }
+  __device__ __forceinline__ bool re_lt(int k, uint32_t cat) const { return ((s.rb[cell(k)] >> 10) & 3u) < cat; }
+
+  // Rand decision bits of one forward for this thread's cells: from injected
+  // fields (src = [3, H, W] float32) or Philox (one 4x32 draw per cell).
+  __device__ __forceinline__ void fill_rands(const float* __restrict__ src, uint32_t k0, uint32_t k1, uint64_t env, uint32_t ep,
+                             uint32_t slot) const {
+#pragma unroll 2
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
+      float rm, ri, re;
       if (src) {
-        rm[k] = src[i];
-        ri[k] = src[C + i];
-        re[k] = src[2 * C + i];
+        rm = src[i];
+        ri = src[C + i];
+        re = src[2 * C + i];
       } else {
         const u32x4 w = philox4x32_10({(uint32_t)i, (uint32_t)env, ep, slot}, k0 ^ (uint32_t)(env >> 32), k1);
-        rm[k] = u01f_from(w.x);
-        ri[k] = u01f_from(w.y);
-        re[k] = u01f_from(w.z);
+        rm = u01f_from(w.x);
+        ri = u01f_from(w.y);
+        re = u01f_from(w.z);
       }
+      s.rb[i] = (uint16_t)rand_bits(rm, ri, re);
     }
   }
 
-  __device__ void forward_rand(const float* __restrict__ src, uint32_t k0, uint32_t k1, uint64_t env, uint32_t ep,
+  __device__ __forceinline__ void forward_rand(const float* __restrict__ src, uint32_t k0, uint32_t k1, uint64_t env, uint32_t ep,
                                uint32_t slot) const {
-    float rm[CPT], ri[CPT], re[CPT];
-    rands(src, k0, k1, env, ep, slot, rm, ri, re);
-    forward(rm, ri, re);
+    const uint32_t P = presence();
+    if (P & kRandUsers) fill_rands(src, k0, k1, env, ep, slot);  // own cells; presence() synced already
+    sync();
+    forward_masked(P);
   }
 
   // HBM <-> LDS for one env's state (bytes, momentum, velocity)
-  __device__ void load(const uint8_t* __restrict__ a, const int8_t* __restrict__ m,
+  __device__ __forceinline__ void load(const uint8_t* __restrict__ a, const int8_t* __restrict__ m,
                        const float2* __restrict__ v) const {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -527,7 +623,7 @@ struct FullWorld {
       s.v[i] = v[i];
     }
   }
-  __device__ void store(uint8_t* __restrict__ a, int8_t* __restrict__ m, float2* __restrict__ v) const {
+  __device__ __forceinline__ void store(uint8_t* __restrict__ a, int8_t* __restrict__ m, float2* __restrict__ v) const {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
@@ -537,13 +633,13 @@ struct FullWorld {
     }
   }
   // goal ids <- current ids
-  __device__ void keep_goal() const {
+  __device__ __forceinline__ void keep_goal() const {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) s.g[cell(k)] = (uint8_t)fid(s.a[cell(k)]);
   }
 
   // Goal mismatch count against s.g (powderworld_env.py:410-418); block total.
-  __device__ int errors() const {
+  __device__ __forceinline__ int errors() const {
     int err = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -556,7 +652,9 @@ struct FullWorld {
     for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
     if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = err;
     sync();
-    const int total = s.red[0] + s.red[1] + s.red[2] + s.red[3];
+    int total = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) total += s.red[w];
     sync();
     return total;
   }
@@ -579,58 +677,120 @@ struct FullWorld {
   }
 
   // Observation: RGB of the world + action frame (powderworld_env.py:462-476),
-  // staged in LDS and written as 16-byte stores.  rgb_only: 3 channels.
-  __device__ void observe(uint8_t* __restrict__ dst, int stage, uint32_t acol, int rx, int brush,
-                          bool rgb_only = false) const {
-    constexpr int NWD = CPT * 6 / 4;
-    uint32_t words[NWD];
-#pragma unroll
-    for (int q = 0; q < NWD; ++q) words[q] = 0;
-#pragma unroll
+  // staged in LDS (6 bytes per cell as three 16-bit stores) and written as
+  // 16-byte stores.  rgb_only: 3 channels.
+  __device__ __forceinline__ void observe(uint8_t* __restrict__ dst, int stage, uint32_t acol, int rx, int brush,
+                                          bool rgb_only = false) const {
+    const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
+    const uint32_t px = fr ? acol : 0u;
+    sync();  // staging shares LDS with the rule scratch
+    uint16_t* st = reinterpret_cast<uint16_t*>(s.ob);
+#pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k), c = c0 + k;
-      const uint32_t col = rgb(fid(s.a[i]), s.v[i]);
-      const bool fr = stage == 1 || (stage == 2 && c >= rx && c < rx + brush);
-      const uint32_t px = fr ? acol : 0u;
-#pragma unroll
-      for (int ch = 0; ch < 6; ++ch) {
-        const int p = 6 * k + ch;
-        const uint32_t b = ch < 3 ? (col >> (8 * ch)) & 0xffu : (px >> (8 * (ch - 3))) & 0xffu;
-        words[p >> 2] |= b << (8 * (p & 3));
-      }
+      const int i = cell(k);
+      const uint32_t c = rgb(fid(s.a[i]), s.v[i]);
+      st[3 * i] = (uint16_t)(c & 0xffffu);
+      st[3 * i + 1] = (uint16_t)(((c >> 16) & 0xffu) | ((px & 0xffu) << 8));
+      st[3 * i + 2] = (uint16_t)((px >> 8) & 0xffffu);
     }
-    sync();  // staging buffer free
-    uint32_t* st = s.ob + threadIdx.x * NWD;
-#pragma unroll
-    for (int q = 0; q < NWD; ++q) st[q] = words[q];
     sync();
     if (!rgb_only) {
       const uint4* src = reinterpret_cast<const uint4*>(s.ob);
       uint4* d = reinterpret_cast<uint4*>(dst);
-      for (int q = threadIdx.x; q < C * 6 / 16; q += 256) d[q] = src[q];
+      for (int q = threadIdx.x; q < C * 6 / 16; q += NT) d[q] = src[q];
     } else {
       const uint8_t* src = reinterpret_cast<const uint8_t*>(s.ob);
-      for (int q = threadIdx.x; q < C * 3; q += 256) dst[q] = src[(q / 3) * 6 + q % 3];
+      for (int q = threadIdx.x; q < C * 3; q += NT) dst[q] = src[(q / 3) * 6 + q % 3];
     }
+    sync();  // staging shares LDS with the rule scratch
   }
 
-  __device__ void forward(const float* rm, const float* ri, const float* re) const {
-    stone();
-    gravity();
-    sand(rm);
-    fluid(rm);
-    ice(ri);
-    water(re);
-    fire(ri, re);
-    plant(ri);
-    velocity();
-  }
-
-  // brush paint of own cells (powderworld_env.py:380-391)
-  __device__ void paint(int elem_id, int rx, int ry, int brush) const {
+  // Bitmask of the ids present in the world (+ kVelBit if some velocity is
+  // nonzero).  A rule whose trigger elements are absent is an identity and is
+  // skipped; the mask is then widened by what each executed rule can create.
+  __device__ __forceinline__ uint32_t presence() const {
+    uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int c = c0 + k;
+      const int i = cell(k);
+      const float2 v = s.v[i];
+      m |= bit((int)fid(s.a[i])) | ((v.x != 0.0f || v.y != 0.0f) ? kVelBit : 0u);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off);
+    sync();  // red is free
+    if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = (int32_t)m;
+    sync();
+    uint32_t all = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) all |= (uint32_t)s.red[w];
+    return all;
+  }
+
+  // OR of a per-thread mask over the workgroup
+  __device__ __forceinline__ uint32_t block_or(uint32_t m) const {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off);
+    if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = (int32_t)m;
+    sync();
+    uint32_t all = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) all |= (uint32_t)s.red[w];
+    sync();  // red is free again
+    return all;
+  }
+
+  // fluid flow can only move cells if one of these is present (own fluid
+  // heavier than a gravity side: water/gas/lava/acid, empty beside gas or
+  // fire, the air animals)
+  static constexpr uint32_t kFluidTrig =
+      bit(kWater) | bit(kGas) | bit(kFire) | bit(kLava) | bit(kAcid) | bit(kKangaroo) | bit(kLemming);
+  static constexpr uint32_t kRandUsers = bit(kSand) | bit(kDust) | kFluidTrig | bit(kIce) | bit(kFire) |
+                                         bit(kLava) | bit(kPlant) | bit(kWater);
+
+  __device__ __forceinline__ void forward_masked(uint32_t P) const {
+#ifdef OGBX_PWF_RULES  // ablation builds (scripts/build_variants.sh): run only the rules in the mask
+    P &= (OGBX_PWF_RULES & 1 ? ~0u : ~bit(kStone));
+    if (!(OGBX_PWF_RULES & 4)) P &= ~(bit(kSand) | bit(kDust));
+    if (!(OGBX_PWF_RULES & 8)) P &= ~kFluidTrig;
+    if (!(OGBX_PWF_RULES & 16)) P &= ~bit(kIce);
+    if (!(OGBX_PWF_RULES & 64)) P &= ~(bit(kFire) | bit(kLava));
+    if (!(OGBX_PWF_RULES & 128)) P &= ~bit(kPlant);
+    if (!(OGBX_PWF_RULES & 256)) P &= ~kVelBit;
+#endif
+    if (P & bit(kStone)) stone();
+    gravity();
+    if (P & (bit(kSand) | bit(kDust))) sand();
+    if (P & kFluidTrig) {
+      fluid();
+    } else {
+      // no move possible: the new momentum of every fluid cell is 0
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) {
+        const uint32_t id = fid(s.a[cell(k)]);
+        if (is_fluid(id) || id == kKangaroo || id == kLemming) s.m[cell(k)] = 0;
+      }
+      sync();
+    }
+    if (P & bit(kIce)) {
+      ice();
+      P |= bit(kWater);
+    }
+    if ((P & bit(kWater)) && (P & bit(kIce))) water();
+    if (P & (bit(kFire) | bit(kLava))) {
+      fire();
+      P |= bit(kFire) | bit(kWater) | bit(kEmpty) | kVelBit;
+    }
+    if (P & bit(kPlant)) plant();
+    if (P & kVelBit) velocity();
+  }
+
+
+  // brush paint of own cells (powderworld_env.py:380-391)
+  __device__ __forceinline__ void paint(int elem_id, int rx, int ry, int brush) const {
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int r = row(k), c = col;
       if (r >= ry && r < ry + brush && c >= rx && c < rx + brush && fid(s.a[cell(k)]) != kWall)
         put(cell(k), elem((uint32_t)elem_id));
     }
