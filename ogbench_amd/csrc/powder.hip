@@ -530,8 +530,11 @@ __global__ void __launch_bounds__(256) pw_forward_kernel(const PowderParams* __r
 // Full-rule worlds (powder_full.h): the state lives in LDS for the whole
 // launch; goal worlds are replayed per env (the forward is stochastic).
 // 1024 threads per 64x64 world, 256 per 32x32 (4 cells per thread).
+#ifndef OGBX_PWF_NT64
+#define OGBX_PWF_NT64 1024  // threads per 64x64 world
+#endif
 template <int WS>
-constexpr int pwf_nt() { return WS == 64 ? 1024 : 256; }
+constexpr int pwf_nt() { return WS == 64 ? OGBX_PWF_NT64 : 256; }
 #ifndef OGBX_PWF_WAVES
 #define OGBX_PWF_WAVES 4  // waves per SIMD the register budget is sized for
 #endif
@@ -645,6 +648,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   __syncthreads();
   const int len = Pp->seq_len[task - 1];
   for (int k = 0; k < k_steps; ++k) {
+    fw.fence_idx();
     const int64_t o = (int64_t)k * n + e;
     const int act = action[o];
     int stage = ctrl & 3, elem = (ctrl >> 2) & 63, x = (ctrl >> 8) & 255, y = 0;
@@ -688,6 +692,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     };
     if (!fw_step) finish_step();
     for (; op <= op_end; ++op) {
+      fw.fence_idx();
       if (op < 0) {
         fw.forward_rand(rand ? rand + (size_t)o * 3 * C : nullptr, r0, r1, e, ep, kRandStep | el_step);
         fw.paint(sh.elem_ids[elem], x * grid, y * grid, brush);

@@ -92,10 +92,14 @@ struct FullWorld {
   static constexpr int H = WS, W = WS, C = WS * WS, CPT = C / NT, RPK = NT / W;
   static_assert(NT % W == 0 && CPT * RPK == H, "whole rows per slab");
   PwFullShared<WS>& s;
-  int r0, col;
+  mutable int r0, col;
   __device__ __forceinline__ explicit FullWorld(PwFullShared<WS>& sh)
       : s(sh), r0((int)threadIdx.x / W), col((int)threadIdx.x % W) {}
 
+  // Opaque redefinition of the thread's coordinates: cell/neighbour indices are
+  // recomputed after it instead of being hoisted (as VGPRs) across the whole
+  // forward by loop-invariant code motion.
+  __device__ __forceinline__ void fence_idx() const { asm volatile("" : "+v"(r0), "+v"(col)); }
   __device__ __forceinline__ int row(int k) const { return r0 + k * RPK; }
   __device__ __forceinline__ int cell(int k) const { return row(k) * W + col; }
   // periodic neighbour (np.roll semantics)
@@ -146,6 +150,7 @@ struct FullWorld {
   }
   __device__ __forceinline__ void stage_from(int i, int j) const { stage(i, s.a[j], s.m[j], s.v[j]); }
   __device__ __forceinline__ void commit() const {
+    fence_idx();
     sync();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
@@ -158,6 +163,7 @@ struct FullWorld {
   }
   // element conversions: f1[i] = new id + 1 (0 = unchanged) -> own cells
   __device__ __forceinline__ void commit_conversions() const {
+    fence_idx();
     sync();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
@@ -169,6 +175,7 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void stone() const {
+    fence_idx();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
@@ -195,6 +202,7 @@ struct FullWorld {
     return (fdens(b) - fdens(a) < 0.0f) && fgrav(a) && fgrav(b);
   }
   __device__ __forceinline__ void gravity() const {
+    fence_idx();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k), up = nb(k, -1, 0), up2 = nb(k, -2, 0), dn = nb(k, 1, 0);
@@ -211,6 +219,7 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void sand() const {
+    fence_idx();
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       const int go = pass == 0 ? -1 : 1;        // fall toward -1 (left) then +1 (right)
@@ -251,6 +260,7 @@ struct FullWorld {
     return match && elem && (!fdidg(a) || air) && (fdens(a) - fdens(sd) > 0.0f) && fgrav(sd) && fgrav(a);
   }
   __device__ __forceinline__ void fluid() const {
+    fence_idx();
     int8_t* mom2 = reinterpret_cast<int8_t*>(s.f1);
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
@@ -292,6 +302,7 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void ice() const {
+    fence_idx();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
@@ -303,6 +314,7 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void water() const {
+    fence_idx();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
@@ -319,6 +331,7 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void fire() const {
+    fence_idx();
     // f1 bit 0: burns (pushes its 4 neighbours with 8), bit 1: dust near fire
     // (pushes with 30), bit 2: fire or lava before the burn; f2: conversion
 #pragma unroll 1
@@ -403,6 +416,7 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void plant() const {
+    fence_idx();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
@@ -429,9 +443,11 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void velocity() const {
+    fence_idx();
     const float inv2pi = (float)(1.0 / (2.0 * 3.141592653589793));
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
+      fence_idx();
       // f2 = angle bin of cells that may move (mag above the pass threshold, not
       // wall), 0xFF otherwise; sw = chosen swap direction (-1 none)
       uint32_t dirs = 0;  // angle bins present among the cells that may move
@@ -473,6 +489,7 @@ struct FullWorld {
 #pragma unroll 1
       for (int d = 0; d < 8; ++d) {
         if (!((dirs >> d) & 1u)) continue;
+        fence_idx();
         int dr, dc;
         dir_of(d, dr, dc);
 #pragma unroll 1
@@ -525,6 +542,7 @@ struct FullWorld {
     }
     sync();
     const float w18 = 1.0f / 18.0f;
+    fence_idx();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {
       float tx[9], ty[9];
@@ -549,6 +567,7 @@ struct FullWorld {
   // ------------------------------------------------------------- env helpers
   // Blank world: walls on the border, empty inside (powderworld_env.py:309-313).
   __device__ __forceinline__ void blank() const {
+    fence_idx();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int r = row(k), c = col;
@@ -586,6 +605,7 @@ struct FullWorld {
   // fields (src = [3, H, W] float32) or Philox (one 4x32 draw per cell).
   __device__ __forceinline__ void fill_rands(const float* __restrict__ src, uint32_t k0, uint32_t k1, uint64_t env, uint32_t ep,
                              uint32_t slot) const {
+    fence_idx();
 #pragma unroll 2
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
@@ -615,6 +635,7 @@ struct FullWorld {
   // HBM <-> LDS for one env's state (bytes, momentum, velocity)
   __device__ __forceinline__ void load(const uint8_t* __restrict__ a, const int8_t* __restrict__ m,
                        const float2* __restrict__ v) const {
+    fence_idx();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
@@ -624,6 +645,7 @@ struct FullWorld {
     }
   }
   __device__ __forceinline__ void store(uint8_t* __restrict__ a, int8_t* __restrict__ m, float2* __restrict__ v) const {
+    fence_idx();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
@@ -634,12 +656,14 @@ struct FullWorld {
   }
   // goal ids <- current ids
   __device__ __forceinline__ void keep_goal() const {
+    fence_idx();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) s.g[cell(k)] = (uint8_t)fid(s.a[cell(k)]);
   }
 
   // Goal mismatch count against s.g (powderworld_env.py:410-418); block total.
   __device__ __forceinline__ int errors() const {
+    fence_idx();
     int err = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -681,6 +705,7 @@ struct FullWorld {
   // 16-byte stores.  rgb_only: 3 channels.
   __device__ __forceinline__ void observe(uint8_t* __restrict__ dst, int stage, uint32_t acol, int rx, int brush,
                                           bool rgb_only = false) const {
+    fence_idx();
     const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
     const uint32_t px = fr ? acol : 0u;
     sync();  // staging shares LDS with the rule scratch
@@ -709,6 +734,7 @@ struct FullWorld {
   // nonzero).  A rule whose trigger elements are absent is an identity and is
   // skipped; the mask is then widened by what each executed rule can create.
   __device__ __forceinline__ uint32_t presence() const {
+    fence_idx();
     uint32_t m = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -788,6 +814,7 @@ struct FullWorld {
 
   // brush paint of own cells (powderworld_env.py:380-391)
   __device__ __forceinline__ void paint(int elem_id, int rx, int ry, int brush) const {
+    fence_idx();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int r = row(k), c = col;
