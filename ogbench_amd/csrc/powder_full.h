@@ -152,7 +152,7 @@ struct FullWorld {
   __device__ __forceinline__ void commit() const {
     fence_idx();
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       s.a[i] = s.a2[i];
@@ -165,7 +165,7 @@ struct FullWorld {
   __device__ __forceinline__ void commit_conversions() const {
     fence_idx();
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t to = s.f1[i];
@@ -176,7 +176,7 @@ struct FullWorld {
 
   __device__ __forceinline__ void stone() const {
     fence_idx();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       uint32_t a = s.a[i];
@@ -188,7 +188,7 @@ struct FullWorld {
       s.a2[i] = (uint8_t)a;
     }
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) s.a[cell(k)] = s.a2[cell(k)];
     sync();
   }
@@ -203,7 +203,7 @@ struct FullWorld {
   }
   __device__ __forceinline__ void gravity() const {
     fence_idx();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k), up = nb(k, -1, 0), up2 = nb(k, -2, 0), dn = nb(k, 1, 0);
       const bool d0 = dbb(i, dn), d1 = dbb(up, i), d2 = dbb(up2, up);
@@ -224,7 +224,7 @@ struct FullWorld {
     for (int pass = 0; pass < 2; ++pass) {
       const int go = pass == 0 ? -1 : 1;        // fall toward -1 (left) then +1 (right)
       const uint32_t fl = pass == 0 ? 1u : 0u;  // fall_dir: rm > 0.5, then rm <= 0.5
-#pragma unroll 1
+#pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), ibl = nb(k, 1, go), iar = nb(k, -1, -go);
         const uint32_t a = s.a[i], bl = s.a[ibl], ar = s.a[iar];
@@ -261,19 +261,23 @@ struct FullWorld {
   }
   __device__ __forceinline__ void fluid() const {
     fence_idx();
-    int8_t* mom2 = reinterpret_cast<int8_t*>(s.f1);
+    int8_t* mom2 = reinterpret_cast<int8_t*>(s.cnt);  // new momentum after pass 2
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       const int go = pass == 0 ? -1 : 1;
-#pragma unroll 1
+      fence_idx();
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) {
+        const int i = cell(k);
+        s.f1[i] = fluid_mv(i, nb(k, 0, go), pass, pass == 0 ? 0 : s.sw[i]);
+      }
+      sync();
+#pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), sd = nb(k, 0, go), b1 = nb(k, 0, -go), b2 = nb(k, 0, -2 * go);
-        const int mom_i = pass == 0 ? 0 : s.sw[i], mom_b1 = pass == 0 ? 0 : s.sw[b1];
-        const int mom_b2 = pass == 0 ? 0 : s.sw[b2];
-        const bool mv0 = fluid_mv(i, sd, pass, mom_i), mv1 = fluid_mv(b1, i, pass, mom_b1);
-        const bool mv2 = fluid_mv(b2, b1, pass, mom_b2);
-        const bool real = mv0 && !mv1, real_in = mv1 && !mv2;
-        const int nm = mom_i + (real_in ? (pass == 0 ? 2 : -2) : 0);
+        const bool mv1 = s.f1[b1];
+        const bool real = s.f1[i] && !mv1, real_in = mv1 && !s.f1[b2];
+        const int nm = (pass == 0 ? 0 : s.sw[i]) + (real_in ? (pass == 0 ? 2 : -2) : 0);
         if (pass == 0) {
           s.f2[i] = (uint8_t)nm;  // staged: sw is read by the neighbours this pass
         } else {
@@ -282,7 +286,7 @@ struct FullWorld {
         stage_from(i, real ? sd : (real_in ? b1 : i));
       }
       sync();
-#pragma unroll 1
+#pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
         s.a[i] = s.a2[i];
@@ -292,7 +296,7 @@ struct FullWorld {
       }
       sync();
     }
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
@@ -303,7 +307,7 @@ struct FullWorld {
 
   __device__ __forceinline__ void ice() const {
     fence_idx();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
       bool to = id == kIce && ri_lt(k, kRi002);
@@ -315,7 +319,7 @@ struct FullWorld {
 
   __device__ __forceinline__ void water() const {
     fence_idx();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
       bool to = id == kWater && re_lt(k, kRe005);
@@ -330,44 +334,50 @@ struct FullWorld {
            x == kMole || x == kLemming;
   }
 
+  // BehaviorFire (sim.py:700-790).  The 3x3 neighbourhood scans are evaluated
+  // only in the lanes whose outcome depends on them (burn candidates, cells
+  // that were fire/lava, fire that may fade, empty cells that may ignite).
   __device__ __forceinline__ void fire() const {
     fence_idx();
     // f1 bit 0: burns (pushes its 4 neighbours with 8), bit 1: dust near fire
     // (pushes with 30), bit 2: fire or lava before the burn; f2: conversion
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
       const bool fl = id == kFire || id == kLava;
-      const bool near = box(k, [](uint32_t x) { return x == kFire || x == kLava; }) > 0;
       const bool p005 = ri_lt(k, kRi005), p02 = ri_lt(k, kRi02);
-      const bool burn = ((id == kWood && p005) || (id == kPlant && p02) || (id == kGas && p02) || id == kDust ||
-                         (id == kBird && p005) ||
-                         ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p02)) &&
-                        near;
-      const bool burn_ice = id == kIce && p02 && near;
+      const bool cand = (id == kWood && p005) || (id == kPlant && p02) || (id == kGas && p02) || id == kDust ||
+                        (id == kBird && p005) ||
+                        ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p02);
+      const bool cand_ice = id == kIce && p02;
+      bool near = false;
+      if (cand || cand_ice) near = box(k, [](uint32_t x) { return x == kFire || x == kLava; }) > 0;
+      const bool burn = cand && near, burn_ice = cand_ice && near;
       s.f1[i] = (uint8_t)((burn ? 1 : 0) | (id == kDust && near ? 2 : 0) | (fl ? 4 : 0));
       s.f2[i] = burn ? kFire + 1 : (burn_ice ? kWater + 1 : 0);
     }
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       float2 v = s.v[i];
       // impulses away from a burning neighbour (sim.py:744-752): left, above, below, right
       const uint32_t L = s.f1[nb(k, 0, -1)], U = s.f1[nb(k, -1, 0)], D = s.f1[nb(k, 1, 0)], R = s.f1[nb(k, 0, 1)];
-      v.y = v.y + 8.0f * (float)(L & 1);
-      v.x = v.x + 8.0f * (float)(U & 1);
-      v.x = v.x - 8.0f * (float)(D & 1);
-      v.y = v.y - 8.0f * (float)(R & 1);
-      v.y = v.y + 30.0f * (float)((L >> 1) & 1);
-      v.x = v.x + 30.0f * (float)((U >> 1) & 1);
-      v.x = v.x - 30.0f * (float)((D >> 1) & 1);
-      v.y = v.y - 30.0f * (float)((R >> 1) & 1);
+      if ((L | U | D | R) & 3u) {
+        v.y = v.y + 8.0f * (float)(L & 1);
+        v.x = v.x + 8.0f * (float)(U & 1);
+        v.x = v.x - 8.0f * (float)(D & 1);
+        v.y = v.y - 8.0f * (float)(R & 1);
+        v.y = v.y + 30.0f * (float)((L >> 1) & 1);
+        v.x = v.x + 30.0f * (float)((U >> 1) & 1);
+        v.x = v.x - 30.0f * (float)((D >> 1) & 1);
+        v.y = v.y - 30.0f * (float)((R >> 1) & 1);
+      }
       s.v2[i] = v;
     }
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t to = s.f2[i];
@@ -379,15 +389,19 @@ struct FullWorld {
     }
     sync();
     // fire spread from (fire or lava before the burn) x burnable neighbours, and lava
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
-      const int nbr = box(k, [](uint32_t x) { return burnable(x); });
-      s.cnt[i] = (int16_t)(nbr * ((s.f1[i] >> 2) & 1) + (fid(s.a[i]) == kLava ? 1 : 0));
+      const uint32_t id = fid(s.a[i]);
+      const bool fl = (s.f1[i] >> 2) & 1;
+      const bool re04 = re_lt(k, kRe04);
+      const bool need = fl || (id == kFire && re04) || (id == kEmpty && re04 && ri_lt(k, kRi03));
+      const int nbr = need ? box(k, [](uint32_t x) { return burnable(x); }) : 1;
+      s.cnt[i] = (int16_t)((fl ? nbr : 0) + (id == kLava ? 1 : 0));
       s.f2[i] = (uint8_t)(nbr == 0);
     }
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
@@ -406,7 +420,7 @@ struct FullWorld {
       s.sw[i] = (int8_t)(fade ? kEmpty + 1 : (burn_empty ? kFire + 1 : 0));
     }
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const int to = s.sw[i];
@@ -417,17 +431,17 @@ struct FullWorld {
 
   __device__ __forceinline__ void plant() const {
     fence_idx();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
+      const bool grow = id == kWater && ri_lt(k, kRi005);
+      const bool seed = id == kEmpty && ri_lt(k, kRi02);
       int to = 0;
-      if (id == kWater || id == kEmpty) {
+      if (grow || seed) {  // the only cells whose outcome depends on the neighbourhood
         const int cnt = box(k, [](uint32_t x) { return x == kPlant; });
-        const bool grow = id == kWater && ri_lt(k, kRi005);
         bool to_plant = grow && cnt <= 3 && cnt >= 1;
         const bool to_empty = grow && cnt > 3;
-        if (!to_plant && id == kEmpty && ri_lt(k, kRi02) && cnt > 0)
-          to_plant = box(k, [](uint32_t x) { return x == kIce || x == kWood; }) > 0;
+        if (seed && cnt > 0) to_plant = box(k, [](uint32_t x) { return x == kIce || x == kWood; }) > 0;
         to = to_plant ? kPlant + 1 : (to_empty ? kEmpty + 1 : 0);
       }
       s.f1[cell(k)] = (uint8_t)to;
@@ -451,7 +465,7 @@ struct FullWorld {
       // f2 = angle bin of cells that may move (mag above the pass threshold, not
       // wall), 0xFF otherwise; sw = chosen swap direction (-1 none)
       uint32_t dirs = 0;  // angle bins present among the cells that may move
-#pragma unroll 1
+#pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
         const float2 v = s.v[i];
@@ -472,7 +486,7 @@ struct FullWorld {
       dirs = block_or(dirs);
       if (dirs == 0) {
         // no swap anywhere: v = v * 0.5 + v * 0.5 in place
-#pragma unroll 1
+#pragma unroll
         for (int k = 0; k < CPT; ++k) {
           float2 v = s.v[cell(k)];
           v.x = v.x * 0.5f + v.x * 0.5f;
@@ -492,13 +506,13 @@ struct FullWorld {
         fence_idx();
         int dr, dc;
         dir_of(d, dr, dc);
-#pragma unroll 1
+#pragma unroll
         for (int k = 0; k < CPT; ++k) {
           const int i = cell(k), j = nb(k, dr, dc);
           s.f1[i] = s.f2[i] == d && cur[i] == -1 && cur[j] == -1 && fid(s.a[j]) == kEmpty;
         }
         sync();
-#pragma unroll 1
+#pragma unroll
         for (int k = 0; k < CPT; ++k) {
           const int i = cell(k);
           int8_t w = cur[i];
@@ -512,11 +526,11 @@ struct FullWorld {
         nxt = t;
       }
       if (cur != s.sw) {
-#pragma unroll 1
+#pragma unroll
         for (int k = 0; k < CPT; ++k) s.sw[cell(k)] = cur[cell(k)];
         sync();
       }
-#pragma unroll 1
+#pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
         const int w = s.sw[i];
@@ -532,7 +546,7 @@ struct FullWorld {
       commit();
     }
     // decay and 3x3 blur (zero padded), NumPy's einsum summation order
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       float2 v = s.v[i];
@@ -543,7 +557,7 @@ struct FullWorld {
     sync();
     const float w18 = 1.0f / 18.0f;
     fence_idx();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       float tx[9], ty[9];
 #pragma unroll
@@ -559,7 +573,7 @@ struct FullWorld {
       s.v2[cell(k)] = make_float2(bx + own.x * 0.5f, by + own.y * 0.5f);
     }
     sync();
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) s.v[cell(k)] = s.v2[cell(k)];
     sync();
   }
@@ -710,7 +724,7 @@ struct FullWorld {
     const uint32_t px = fr ? acol : 0u;
     sync();  // staging shares LDS with the rule scratch
     uint16_t* st = reinterpret_cast<uint16_t*>(s.ob);
-#pragma unroll 1
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t c = rgb(fid(s.a[i]), s.v[i]);

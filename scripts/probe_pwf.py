@@ -16,13 +16,19 @@ for level in ('medium', 'hard'):
     n, size = 4096, 64
     ne = 5 if level == 'medium' else 8
     env = ogbench_amd.make(f'powderworld-{level}-v0', num_envs=n, device=dev, world_size=size)
-    env.reset(seed=1, options=dict(task_id=(torch.arange(n, device=dev) % 5 + 1)))
-    rng = np.random.RandomState(0)
-    xy = env._xy_action_size
-    K = 150
-    acts = np.stack([rng.randint(0, ne if t % 3 == 0 else xy, size=n) for t in range(K)])
-    env.rollout(acts)
-    w = env.world_full().contiguous()
+    cache = os.path.join('gpurun_out', f'pwf_worlds_{level}.pt')  # same worlds for every build variant
+    if os.path.exists(cache):
+        w = torch.load(cache, weights_only=True).to(dev)
+    else:
+        env.reset(seed=1, options=dict(task_id=(torch.arange(n, device=dev) % 5 + 1)))
+        rng = np.random.RandomState(0)
+        xy = env._xy_action_size
+        K = 150
+        acts = np.stack([rng.randint(0, ne if t % 3 == 0 else xy, size=n) for t in range(K)])
+        env.rollout(acts)
+        w = env.world_full().contiguous()
+        os.makedirs('gpurun_out', exist_ok=True)
+        torch.save(w.cpu(), cache)
     env.forward_full(w, 1)
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
