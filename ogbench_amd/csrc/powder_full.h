@@ -79,6 +79,9 @@ __device__ __forceinline__ uint32_t fid(uint32_t a) { return a & 31u; }
 __device__ __forceinline__ uint32_t fgrav(uint32_t a) { return (a >> 5) & 1u; }
 __device__ __forceinline__ uint32_t fdidg(uint32_t a) { return (a >> 6) & 1u; }
 __device__ __forceinline__ float fdens(uint32_t a) { return (float)((kDensPacked >> (3u * (a & 31u))) & 7u); }
+// density as an integer: float32 differences of these small integers compare
+// exactly like the integers, so the rules compare dens_i directly
+__device__ __forceinline__ uint32_t dens_i(uint32_t a) { return (uint32_t)(kDensPacked >> (3u * (a & 31u))) & 7u; }
 
 constexpr uint32_t bit(int id) { return 1u << id; }
 constexpr uint32_t kVelBit = 1u << 31;  // presence mask: some velocity is nonzero
@@ -104,15 +107,13 @@ struct FullWorld {
   __device__ __forceinline__ int cell(int k) const { return row(k) * W + col; }
   // periodic neighbour (np.roll semantics)
   __device__ __forceinline__ int nb(int k, int dr, int dc) const {
-    int rr = row(k) + dr, cc = col + dc;
-    rr = rr < 0 ? rr + H : (rr >= H ? rr - H : rr);
-    cc = cc < 0 ? cc + W : (cc >= W ? cc - W : cc);
-    return rr * W + cc;
+    static_assert((H & (H - 1)) == 0 && (W & (W - 1)) == 0, "power-of-two worlds: wrap by masking");
+    return ((row(k) + dr) & (H - 1)) * W + ((col + dc) & (W - 1));
   }
   // zero-padded neighbour (conv2d padding=1): -1 outside
   __device__ __forceinline__ int zp(int k, int dr, int dc) const {
     const int rr = row(k) + dr, cc = col + dc;
-    return (rr < 0 || rr >= H || cc < 0 || cc >= W) ? -1 : rr * W + cc;
+    return ((unsigned)rr < (unsigned)H && (unsigned)cc < (unsigned)W) ? rr * W + cc : -1;
   }
   __device__ __forceinline__ void sync() const { __syncthreads(); }
 
@@ -136,7 +137,8 @@ struct FullWorld {
 #pragma unroll 1
     for (int q = 0; q < 9; ++q) {  // rolled: keeps the register footprint small
       const int j = zp(k, q / 3 - 1, q % 3 - 1);
-      n += (j >= 0 && pred(fid(s.a[j]))) ? 1 : 0;
+      const uint32_t x = s.a[j >= 0 ? j : 0];  // branch-free: load, then mask
+      n += ((j >= 0) & pred(fid(x))) ? 1 : 0;
     }
     return n;
   }
@@ -182,7 +184,8 @@ struct FullWorld {
       uint32_t a = s.a[i];
       if (fid(a) == kStone) {
         const int jl = zp(k, -1, -1), jr = zp(k, -1, 1);
-        const int sup = (jl >= 0 && fid(s.a[jl]) == kStone) + (jr >= 0 && fid(s.a[jr]) == kStone);
+        const uint32_t al = s.a[jl >= 0 ? jl : 0], ar = s.a[jr >= 0 ? jr : 0];
+        const int sup = ((jl >= 0) & (fid(al) == kStone)) + ((jr >= 0) & (fid(ar) == kStone));
         a = (a & ~kGrav) | (sup < 2 ? kGrav : 0u);
       }
       s.a2[i] = (uint8_t)a;
@@ -199,7 +202,7 @@ struct FullWorld {
   __device__ static __forceinline__ uint32_t rd(uint32_t a) { return fgrav(a) ? (a & ~kDidg) : a; }
   __device__ __forceinline__ bool dbb(int i, int ib) const {
     const uint32_t a = s.a[i], b = s.a[ib];
-    return (fdens(b) - fdens(a) < 0.0f) && fgrav(a) && fgrav(b);
+    return (dens_i(b) < dens_i(a)) & (bool)fgrav(a) & (bool)fgrav(b);
   }
   __device__ __forceinline__ void gravity() const {
     fence_idx();
@@ -207,13 +210,9 @@ struct FullWorld {
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k), up = nb(k, -1, 0), up2 = nb(k, -2, 0), dn = nb(k, 1, 0);
       const bool d0 = dbb(i, dn), d1 = dbb(up, i), d2 = dbb(up2, up);
-      if (d0 && !d1) {
-        stage(i, rd(s.a[dn]), s.m[dn], s.v[dn]);
-      } else if (d1 && !d2) {
-        stage(i, rd(s.a[up]) | kDidg, s.m[up], s.v[up]);
-      } else {
-        stage(i, rd(s.a[i]), s.m[i], s.v[i]);
-      }
+      const bool down = d0 & !d1, raised = d1 & !d2;
+      const int j = down ? dn : (raised ? up : i);
+      stage(i, rd(s.a[j]) | (raised ? kDidg : 0u), s.m[j], s.v[j]);
     }
     commit();
   }
@@ -232,17 +231,16 @@ struct FullWorld {
         const bool elem_ar = fid(ar) == kSand || fid(ar) == kDust;
         const bool ndg = !fdidg(a);
         const bool f_own = (s.rb[i] & 1u) == fl, f_ar = (s.rb[iar] & 1u) == fl;
-        const bool mv = elem && !fdidg(bl) && f_own && (fdens(a) - fdens(bl) > 0.0f) && fgrav(bl) && ndg;
-        const bool in = elem_ar && !fdidg(ar) && f_ar && (fdens(ar) - fdens(a) > 0.0f) && fgrav(ar) && ndg;
+        const bool mv = elem & !fdidg(bl) & f_own & (dens_i(a) > dens_i(bl)) & (bool)fgrav(bl) & ndg;
+        const bool in = elem_ar & !fdidg(ar) & f_ar & (dens_i(ar) > dens_i(a)) & (bool)fgrav(ar) & ndg;
         stage_from(i, mv ? ibl : (in ? iar : i));
       }
       commit();
     }
   }
 
-  __device__ static __forceinline__ bool is_fluid(uint32_t id) {
-    return id == kEmpty || id == kWater || id == kGas || id == kLava || id == kAcid;
-  }
+  static constexpr uint32_t kFluidIds = bit(kEmpty) | bit(kWater) | bit(kGas) | bit(kLava) | bit(kAcid);
+  __device__ static __forceinline__ bool is_fluid(uint32_t id) { return (kFluidIds >> id) & 1u; }
 
   // FluidFlow (sim.py:593-667), two passes (left, then right).  A cell's move
   // decision mv needs only its own state and its side neighbour's, so real
@@ -255,11 +253,15 @@ struct FullWorld {
     // (rm + ch6) + mom > 0.5 for ch6 in {-2, 0, 2}, mom in {0, 2}: rand_bits
     const bool fall = (s.rb[j] >> (1 + m6 + (mom != 0 ? 3 : 0))) & 1u;
     const bool match = pass == 0 ? fall : !fall;
-    const bool air = fid(a) == kKangaroo || fid(a) == kLemming;
-    const bool elem = is_fluid(fid(a)) || air;
-    return match && elem && (!fdidg(a) || air) && (fdens(a) - fdens(sd) > 0.0f) && fgrav(sd) && fgrav(a);
+    const uint32_t id = fid(a);
+    const bool air = (bit(kKangaroo) | bit(kLemming)) >> id & 1u;
+    const bool elem = (kFluidIds >> id) & 1u;
+    return match & elem & (!fdidg(a) | air) & (dens_i(a) > dens_i(sd)) & (bool)fgrav(sd) & (bool)fgrav(a);
   }
   __device__ __forceinline__ void fluid() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; FLUID_BEGIN");
+#endif
     fence_idx();
     int8_t* mom2 = reinterpret_cast<int8_t*>(s.cnt);  // new momentum after pass 2
 #pragma unroll 1
@@ -275,8 +277,8 @@ struct FullWorld {
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), sd = nb(k, 0, go), b1 = nb(k, 0, -go), b2 = nb(k, 0, -2 * go);
-        const bool mv1 = s.f1[b1];
-        const bool real = s.f1[i] && !mv1, real_in = mv1 && !s.f1[b2];
+        const bool mv0 = s.f1[i], mv1 = s.f1[b1], mv2 = s.f1[b2];
+        const bool real = mv0 & !mv1, real_in = mv1 & !mv2;
         const int nm = (pass == 0 ? 0 : s.sw[i]) + (real_in ? (pass == 0 ? 2 : -2) : 0);
         if (pass == 0) {
           s.f2[i] = (uint8_t)nm;  // staged: sw is read by the neighbours this pass
@@ -306,6 +308,9 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void ice() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; ICE_BEGIN");
+#endif
     fence_idx();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -509,7 +514,9 @@ struct FullWorld {
 #pragma unroll
         for (int k = 0; k < CPT; ++k) {
           const int i = cell(k), j = nb(k, dr, dc);
-          s.f1[i] = s.f2[i] == d && cur[i] == -1 && cur[j] == -1 && fid(s.a[j]) == kEmpty;
+          const uint32_t bi = s.f2[i], aj = s.a[j];
+          const int ci = cur[i], cj = cur[j];
+          s.f1[i] = (bi == (uint32_t)d) & (ci == -1) & (cj == -1) & (fid(aj) == kEmpty);
         }
         sync();
 #pragma unroll
