@@ -100,7 +100,7 @@ def _per_launch_ms(fn, launches, dev, host_us=120.0):
     return a.elapsed_time(b) / launches
 
 
-def _traffic(kernel, kern_ms):
+def _traffic(kernel, kern_ms, workload=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/traffic.json, written by scripts/prof_summary.py from separate
     FETCH_SIZE and WRITE_SIZE passes of this same command: bytes = (2 x FETCH_SIZE
@@ -112,6 +112,12 @@ def _traffic(kernel, kern_ms):
             rec = json.load(f).get(kernel)
     except (OSError, ValueError):
         return None
+    if workload is not None:
+        try:
+            with open(path) as f:
+                rec = json.load(f).get(f'{kernel}@{workload}', rec)
+        except (OSError, ValueError):
+            pass
     if not rec:
         return None
     return rec.get('hbm_bytes_per_launch')
@@ -167,8 +173,8 @@ def bench_pointmaze(args, world, rank, dev):
         extra['graph_replay_steps_per_s'] = n * G * reps * world / gdt
     except Exception as e:  # pragma: no cover - reported, not fatal
         extra['graph_replay_error'] = repr(e)[:200]
-    # K fused steps per launch
-    K = 64
+    # K fused steps per launch (K = 1 and K = 100)
+    K = 100
     fused_actions = actions[:K].contiguous()
     out = None
 
@@ -179,11 +185,24 @@ def bench_pointmaze(args, world, rank, dev):
     fused(0)
     reps = max(1, args.steps // K)
     fdt = _timed(fused, reps, world, dev)
-    extra['fused_k64_steps_per_s'] = n * K * reps * world / fdt
+    extra[f'fused_k{K}_steps_per_s'] = n * K * reps * world / fdt
     fk_ms = _per_launch_ms(fused, 5, dev)
     fused_bytes = (8 + 16 + 4 + 3) * n * K + (16 + 16 + 4 + 4 + 16 + 4 + 4) * n
-    extra['fused_k64_kernel_ms'] = fk_ms
-    extra['fused_k64_achieved_GBs'] = fused_bytes / (fk_ms * 1e-3) / 1e9
+    extra[f'fused_k{K}_kernel_ms'] = fk_ms
+    extra[f'fused_k{K}_achieved_GBs'] = fused_bytes / (fk_ms * 1e-3) / 1e9
+    if world > 1:
+        # strong scaling beside the weak-scaling value: N = 65,536 envs in total,
+        # n / world per rank (SURVEY section 8e reports both)
+        sn = max(64, n // world)
+        senv = ogbench_amd.make('pointmaze-large-v0', num_envs=sn, device=dev, auto_reset=True)
+        senv.reset(seed=rank, options=dict(task_id=task[:sn]))
+        sact = actions[:, :sn].contiguous()
+        for i in range(args.warmup):
+            senv.step(sact[i % ring])
+        sdt = _timed(lambda i: senv.step(sact[i % ring]), args.steps, world, dev)
+        extra['strong_total_envs'] = sn * world
+        extra['strong_env_steps_per_s'] = sn * args.steps * world / sdt
+        senv.close()
     return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
 
 
@@ -531,7 +550,7 @@ def bench_powder(args, world, rank, dev, level='easy'):
         config=dict(workload=f'powderworld-{level}-v0 world_size=64', num_envs_per_gpu=n, auto_reset=True,
                     parallelism=f'env-shard x{world}'),
         roofline=dict(bound='hbm', kernel=kern, achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic(kern, kern_ms), kernel_ms=kern_ms,
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic(kern, kern_ms, args.workload), kernel_ms=kern_ms,
                       alg_bytes_per_launch=per_step * n),
         extra=extra,
     )

@@ -79,6 +79,7 @@ def main():
         with open(tpath) as f:
             data = json.load(f)
     data[a.kernel] = rec
+    data[f'{a.kernel}@{a.workload}'] = rec  # kernels shared by several workloads (powder medium / hard)
     with open(tpath, 'w') as f:
         json.dump(data, f, indent=1, sort_keys=True)
     print(json.dumps({a.kernel: rec}))
