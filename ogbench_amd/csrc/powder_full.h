@@ -163,6 +163,25 @@ struct FullWorld {
     }
     sync();
   }
+  // Copy back only the cells that moved (bit k of `moved`); the others get
+  // own(i), an in-place update of the cell itself (or nothing).
+  template <typename Own>
+  __device__ __forceinline__ void commit_moved(uint32_t moved, Own own) const {
+    fence_idx();
+    sync();
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int i = cell(k);
+      if ((moved >> k) & 1u) {
+        s.a[i] = s.a2[i];
+        s.m[i] = s.m2[i];
+        s.v[i] = s.v2[i];
+      } else {
+        own(i);
+      }
+    }
+    sync();
+  }
   // element conversions: f1[i] = new id + 1 (0 = unchanged) -> own cells
   __device__ __forceinline__ void commit_conversions() const {
     fence_idx();
@@ -206,15 +225,19 @@ struct FullWorld {
   }
   __device__ __forceinline__ void gravity() const {
     fence_idx();
+    uint32_t moved = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k), up = nb(k, -1, 0), up2 = nb(k, -2, 0), dn = nb(k, 1, 0);
       const bool d0 = dbb(i, dn), d1 = dbb(up, i), d2 = dbb(up2, up);
       const bool down = d0 & !d1, raised = d1 & !d2;
-      const int j = down ? dn : (raised ? up : i);
-      stage(i, rd(s.a[j]) | (raised ? kDidg : 0u), s.m[j], s.v[j]);
+      if (down | raised) {
+        const int j = down ? dn : up;
+        stage(i, rd(s.a[j]) | (raised ? kDidg : 0u), s.m[j], s.v[j]);
+        moved |= 1u << k;
+      }
     }
-    commit();
+    commit_moved(moved, [&](int i) { s.a[i] = (uint8_t)rd(s.a[i]); });
   }
 
   __device__ __forceinline__ void sand() const {
@@ -223,6 +246,7 @@ struct FullWorld {
     for (int pass = 0; pass < 2; ++pass) {
       const int go = pass == 0 ? -1 : 1;        // fall toward -1 (left) then +1 (right)
       const uint32_t fl = pass == 0 ? 1u : 0u;  // fall_dir: rm > 0.5, then rm <= 0.5
+      uint32_t moved = 0;
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), ibl = nb(k, 1, go), iar = nb(k, -1, -go);
@@ -233,9 +257,12 @@ struct FullWorld {
         const bool f_own = (s.rb[i] & 1u) == fl, f_ar = (s.rb[iar] & 1u) == fl;
         const bool mv = elem & !fdidg(bl) & f_own & (dens_i(a) > dens_i(bl)) & (bool)fgrav(bl) & ndg;
         const bool in = elem_ar & !fdidg(ar) & f_ar & (dens_i(ar) > dens_i(a)) & (bool)fgrav(ar) & ndg;
-        stage_from(i, mv ? ibl : (in ? iar : i));
+        if (mv | in) {
+          stage_from(i, mv ? ibl : iar);
+          moved |= 1u << k;
+        }
       }
-      commit();
+      commit_moved(moved, [](int) {});
     }
   }
 
@@ -274,6 +301,7 @@ struct FullWorld {
         s.f1[i] = fluid_mv(i, nb(k, 0, go), pass, pass == 0 ? 0 : s.sw[i]);
       }
       sync();
+      uint32_t moved = 0;
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), sd = nb(k, 0, go), b1 = nb(k, 0, -go), b2 = nb(k, 0, -2 * go);
@@ -285,15 +313,20 @@ struct FullWorld {
         } else {
           mom2[i] = (int8_t)nm;
         }
-        stage_from(i, real ? sd : (real_in ? b1 : i));
+        if (real | real_in) {
+          stage_from(i, real ? sd : b1);
+          moved |= 1u << k;
+        }
       }
       sync();
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
-        s.a[i] = s.a2[i];
-        s.m[i] = s.m2[i];
-        s.v[i] = s.v2[i];
+        if ((moved >> k) & 1u) {
+          s.a[i] = s.a2[i];
+          s.m[i] = s.m2[i];
+          s.v[i] = s.v2[i];
+        }
         if (pass == 0) s.sw[i] = (int8_t)s.f2[i];
       }
       sync();
@@ -537,20 +570,27 @@ struct FullWorld {
         for (int k = 0; k < CPT; ++k) s.sw[cell(k)] = cur[cell(k)];
         sync();
       }
+      uint32_t moved = 0;
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
         const int w = s.sw[i];
-        int j = i;
         if (w >= 0) {
           int dr, dc;
           dir_of(w, dr, dc);
-          j = nb(k, dr, dc);
+          const int j = nb(k, dr, dc);
+          const float2 old = s.v[i], nv = s.v[j];
+          stage(i, s.a[j], s.m[j], make_float2(nv.x * 0.5f + old.x * 0.5f, nv.y * 0.5f + old.y * 0.5f));
+          moved |= 1u << k;
         }
-        const float2 old = s.v[i], nv = s.v[j];
-        stage(i, s.a[j], s.m[j], make_float2(nv.x * 0.5f + old.x * 0.5f, nv.y * 0.5f + old.y * 0.5f));
       }
-      commit();
+      // unswapped cells: v = v * 0.5 + v * 0.5 in place
+      commit_moved(moved, [&](int i) {
+        float2 v = s.v[i];
+        v.x = v.x * 0.5f + v.x * 0.5f;
+        v.y = v.y * 0.5f + v.y * 0.5f;
+        s.v[i] = v;
+      });
     }
     // decay and 3x3 blur (zero padded), NumPy's einsum summation order
 #pragma unroll
