@@ -206,9 +206,10 @@ def bench_pointmaze(args, world, rank, dev):
     return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
 
 
-def _eval_allgather(env, actions, world, dev, steps=200):
+def _eval_allgather(env, actions, world, dev, steps=1000):
     """Untimed: the eval success reduction of SURVEY section 8e -- per-task
-    {success, episodes} counters accumulated on the device for `steps` steps,
+    {success, episodes} counters accumulated on the device for `steps` steps
+    (1000 = the TimeLimit, so every env completes at least one episode),
     then all-gathered over the process group (RCCL over xGMI at N>1)."""
     from ogbench_amd.evaluation import accumulate, env_task_ids, gather_counters, summarize
 
