@@ -224,6 +224,9 @@ struct FullWorld {
     return (dens_i(b) < dens_i(a)) & (bool)fgrav(a) & (bool)fgrav(b);
   }
   __device__ __forceinline__ void gravity() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; GRAV_BEGIN");
+#endif
     fence_idx();
     uint32_t moved = 0;
 #pragma unroll
@@ -241,6 +244,9 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void sand() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; SAND_BEGIN");
+#endif
     fence_idx();
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
@@ -376,6 +382,9 @@ struct FullWorld {
   // only in the lanes whose outcome depends on them (burn candidates, cells
   // that were fire/lava, fire that may fade, empty cells that may ignite).
   __device__ __forceinline__ void fire() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; FIRE_BEGIN");
+#endif
     fence_idx();
     // f1 bit 0: burns (pushes its 4 neighbours with 8), bit 1: dust near fire
     // (pushes with 30), bit 2: fire or lava before the burn; f2: conversion
@@ -468,6 +477,9 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void plant() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; PLANT_BEGIN");
+#endif
     fence_idx();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
@@ -495,6 +507,9 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void velocity() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; VEL_BEGIN");
+#endif
     fence_idx();
     const float inv2pi = (float)(1.0 / (2.0 * 3.141592653589793));
 #pragma unroll 1
@@ -724,6 +739,9 @@ struct FullWorld {
 
   // Goal mismatch count against s.g (powderworld_env.py:410-418); block total.
   __device__ __forceinline__ int errors() const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; ERR_BEGIN");
+#endif
     fence_idx();
     int err = 0;
 #pragma unroll
@@ -766,6 +784,9 @@ struct FullWorld {
   // 16-byte stores.  rgb_only: 3 channels.
   __device__ __forceinline__ void observe(uint8_t* __restrict__ dst, int stage, uint32_t acol, int rx, int brush,
                                           bool rgb_only = false) const {
+#ifdef OGBX_ASM_MARKS
+    asm volatile("; OBS_BEGIN");
+#endif
     fence_idx();
     const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
     const uint32_t px = fr ? acol : 0u;

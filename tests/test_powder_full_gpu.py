@@ -192,3 +192,67 @@ def test_full_errors(gpu):
     easy = ogbench_amd.make('powderworld-easy-v0', num_envs=1, device=gpu)
     with pytest.raises(ValueError):
         easy.step([0], rand=np.zeros((1, 3, 32, 32), np.float32))
+
+
+@pytest.mark.parametrize('ne,size', [(8, 32), (5, 64)])
+def test_fused_rollout_with_auto_reset_matches_single_steps(gpu, ne, size):
+    """Philox mode, auto-reset inside the launch: K steps fused in one launch ==
+    K single-step launches from the same state (outputs and final state)."""
+    n, K = 6, 40
+    a = _env(gpu, n, ne=ne, size=size, max_episode_steps=9, auto_reset=True)
+    b = _env(gpu, n, ne=ne, size=size, max_episode_steps=9, auto_reset=True)
+    opts = dict(task_id=torch.arange(n, device=gpu) % 5 + 1)
+    a.reset(seed=5, options=opts)
+    b.reset(seed=5, options=opts)
+    rng = np.random.RandomState(4)
+    acts = rng.randint(0, max(ne, a._xy_action_size) + 1, size=(K, n))
+    out = a.rollout(acts)
+    for t in range(K):
+        ob, rew, term, trunc, info = b.step(acts[t])
+        assert torch.equal(out['obs'][t], ob), t
+        assert torch.equal(out['reward'][t], rew), t
+        assert torch.equal(out['truncated'][t].bool(), trunc), t
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in ('world', 'ctrl', 'elapsed', 'episode', 'momentum', 'velocity', 'goal'):
+        assert torch.equal(sa[k], sb[k]), k
+    assert int(out['truncated'].sum()) >= n * 4  # several auto-resets happened in the launch
+
+
+def test_masked_reset_leaves_other_envs(gpu):
+    env = _env(gpu, 4)
+    env.reset(seed=3, options=dict(task_id=2))
+    for t in range(6):
+        env.step(np.full(4, t % 3))
+    before = env.state_dict()
+    mask = torch.tensor([1, 0, 1, 0], dtype=torch.uint8, device=gpu)
+    env.reset(options=dict(task_id=4), mask=mask)
+    after = env.state_dict()
+    for k in ('world', 'momentum', 'velocity', 'goal'):
+        assert torch.equal(after[k][1], before[k][1]) and torch.equal(after[k][3], before[k][3]), k
+        assert not torch.equal(after[k][0], before[k][0]) or k in ('momentum', 'velocity'), k
+    assert env.cur_task_ids.tolist() == [4, 2, 4, 2]
+    assert (env._state_views()[2][[0, 2]] == 0).all()
+
+
+def test_forward_rand_threshold_edges(gpu):
+    """Rand values at and one ulp around every threshold the rules compare
+    against (sand 0.5; fluid (rm + ch6) + mom > 0.5 with its float32 rounding;
+    ice/plant/fire/water thresholds): the kernel's exact reduction of the three
+    fields to decision bits must agree with the reference's float32 arithmetic."""
+    rng = np.random.RandomState(77)
+    f32 = np.float32
+    edges = []
+    for t in (0.5, 0.02, 0.05, 0.2, 0.3, 0.4):
+        t = f32(t)
+        edges += [np.nextafter(t, f32(0)), t, np.nextafter(t, f32(1))]
+    edges += [f32(0.5) + f32(2 ** -24), f32(0.5) - f32(2 ** -25), f32(0.0), np.nextafter(f32(1), f32(0))]
+    edges = np.array(edges, np.float32)
+    n, size, steps = 4, 32, 6
+    w = _seeded_world(rng, n, size, 8)
+    rand = edges[rng.randint(0, len(edges), size=(steps, n, 3, size, size))]
+    env = _env(gpu, 1, ne=8, size=size)
+    got = env.forward_full(w, steps, rand=rand).cpu().numpy()
+    ref = w
+    for t in range(steps):
+        ref = orc.forward(ref, [rand[t][:, k] for k in range(3)])
+    assert np.array_equal(got, ref), _diff(got, ref)
