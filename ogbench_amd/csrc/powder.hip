@@ -7,10 +7,12 @@
 //   PWRenderer.render               sim.py:386-453
 //   PowderworldEnv reset/step/obs   ogbench/powderworld/powderworld_env.py:284-476
 //
-// Scope: the 'easy' element set (empty, wall, plant, stone; num_elems == 2).
-// For those elements the Sand, FluidFlow, Ice, Water, Fire, Plant and Velocity
-// rules are identities (no sand/dust/water/gas/fire/ice/wood, velocity 0), so
-// a forward pass is Stone then Gravity.  medium/hard are rejected at create.
+// Two kernel families.  The 'easy' element set (empty, wall, plant, stone;
+// num_elems == 2): the Sand, FluidFlow, Ice, Water, Fire, Plant and Velocity
+// rules are identities there (no sand/dust/water/gas/fire/ice/wood, velocity
+// 0), so a forward pass is Stone then Gravity, done SWAR on packed bytes
+// below (pw_*_kernel).  Medium/hard (num_elems 5/8) run every rule in LDS
+// with float32 velocities (powder_full.h, pwf_*_kernel).
 //
 // Layout in HBM: world u8[N, H*W], one byte per cell = element id (bits 0-4)
 // | GravityInter (bit 5, channel 2) | DidGravity (bit 6, channel 8); every
