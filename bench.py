@@ -227,8 +227,39 @@ def _eval_allgather(env, actions, world, dev, steps=1000):
     torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t0) * 1e3
     m = summarize(total, env.task_infos)
-    return dict(episodes=int(total[:, 1].sum()), ranks=int(per_rank.shape[0]),
-                overall_success=m.get('evaluation/overall_success'), allgather_ms=ms)
+    res = dict(episodes=int(total[:, 1].sum()), ranks=int(per_rank.shape[0]),
+               overall_success=m.get('evaluation/overall_success'), allgather_ms=ms)
+    if world > 1:
+        res.update(_cabi_allgather_check(counters, per_rank, world, dev))
+    return res
+
+
+def _cabi_allgather_check(counters, per_rank, world, dev):
+    """The same all-gather through the C-ABI communicator (ogbx_comm_* over
+    RCCL, the path a non-Python host binds): must equal torch.distributed's.
+    Reported, never fatal."""
+    import torch.distributed as dist
+
+    from ogbench_amd.evaluation import RcclComm, comm_unique_id
+
+    try:
+        if dist.get_backend() != 'nccl':
+            return {'cabi_allgather': 'skipped (gloo rehearsal: RCCL needs one GPU per rank)'}
+        uid = torch.zeros(128, dtype=torch.uint8, device=dev)
+        if dist.get_rank() == 0:
+            uid.copy_(torch.frombuffer(bytearray(comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        comm = RcclComm(world, dist.get_rank(), dev, bytes(uid.cpu().numpy().tobytes()))
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        out = comm.allgather(counters)
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t0) * 1e3
+        ok = bool(torch.equal(out.to(per_rank.device), per_rank))
+        comm.close()
+        return {'cabi_allgather_ms': ms, 'cabi_allgather_matches': ok}
+    except Exception as e:  # pragma: no cover - reported, not fatal
+        return {'cabi_allgather_error': repr(e)[:200]}
 
 
 def _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env):

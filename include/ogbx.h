@@ -490,6 +490,28 @@ ogbx_status ogbx_eval_accumulate(const uint8_t* success, const uint8_t* terminat
                                  int32_t* remaining, int64_t n, int32_t num_tasks, int64_t* counters,
                                  void* stream);
 
+/* ----------------------------------------------------------------------
+ * Eval all-gather over RCCL (xGMI), for hosts without torch.distributed
+ * (impls/main.py:226-258 gathers per-task success across workers).  One
+ * communicator per (process, device): rank 0 calls ogbx_comm_unique_id and
+ * ships the 128-byte id to every rank out of band (the cgo / JNI host's own
+ * channel); every rank then calls ogbx_comm_create.  RCCL is resolved at
+ * run time (the librccl.so.1 already in the process, e.g. PyTorch's, or the
+ * system one), so libogbx.so has no link-time RCCL dependency.
+ * ---------------------------------------------------------------------- */
+typedef struct ogbx_comm* ogbx_comm_t;
+#define OGBX_COMM_ID_BYTES 128
+
+ogbx_status ogbx_comm_unique_id(uint8_t* id /* host [OGBX_COMM_ID_BYTES] */);
+ogbx_status ogbx_comm_create(const uint8_t* id, int32_t world_size, int32_t rank, int32_t device,
+                             ogbx_comm_t* out);
+ogbx_status ogbx_comm_destroy(ogbx_comm_t comm);
+/* all[r * count + i] = local_of_rank_r[i] for every rank r: device int64
+ * local[count] (e.g. the int64[num_tasks, 2] counters) -> device int64
+ * all[world_size * count].  Async on `stream`. */
+ogbx_status ogbx_eval_allgather(ogbx_comm_t comm, const int64_t* local, int64_t count, int64_t* all,
+                                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

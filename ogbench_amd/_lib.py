@@ -110,6 +110,10 @@ _SIGNATURES = {
     'ogbx_eval_accumulate': (
         c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]
     ),
+    'ogbx_comm_unique_id': (c_int32, [c_void_p]),
+    'ogbx_comm_create': (c_int32, [c_void_p, c_int32, c_int32, c_int32, P(c_void_p)]),
+    'ogbx_comm_destroy': (c_int32, [c_void_p]),
+    'ogbx_eval_allgather': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
 }
 
 _lock = threading.Lock()

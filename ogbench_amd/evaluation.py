@@ -47,16 +47,71 @@ def accumulate(counters, success, terminated, truncated, task_id, remaining):
     )
 
 
-def gather_counters(counters, group=None):
+def comm_unique_id():
+    """RCCL unique id (bytes) for RcclComm; rank 0 creates it and ships it to
+    the other ranks out of band."""
+    buf = (_lib.ctypes.c_uint8 * 128)()
+    _lib.check(_lib.lib().ogbx_comm_unique_id(_lib.ctypes.cast(buf, _lib.c_void_p)), 'comm_unique_id')
+    return bytes(buf)
+
+
+class RcclComm:
+    """An RCCL communicator owned by libogbx (``ogbx_comm_create``): the C-ABI
+    all-gather for hosts that do not run torch.distributed.  Python callers
+    normally use ``gather_counters(counters)`` over the default process group;
+    this path is the same collective bound directly."""
+
+    def __init__(self, world_size, rank, device, unique_id):
+        assert len(unique_id) == 128
+        self.world_size, self.rank = int(world_size), int(rank)
+        self.device = _lib_device(device)
+        buf = (_lib.ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._h = _lib.c_void_p()
+        _lib.check(_lib.lib().ogbx_comm_create(_lib.ctypes.cast(buf, _lib.c_void_p), self.world_size, self.rank,
+                                               self.device.index, self._h), 'comm_create')
+
+    def allgather(self, counters):
+        """int64 device tensor [...] -> [world_size, ...] (every rank's block)."""
+        torch = _torch()
+        local = counters.contiguous()
+        assert local.dtype == torch.int64 and local.is_cuda
+        out = torch.empty((self.world_size,) + tuple(local.shape), dtype=torch.int64, device=local.device)
+        _lib.check(_lib.lib().ogbx_eval_allgather(self._h, _lib.ptr(local), local.numel(), _lib.ptr(out),
+                                                  _lib.stream_of(local.device)), 'eval_allgather')
+        return out
+
+    def close(self):
+        if getattr(self, '_h', None) is not None and self._h.value:
+            _lib.lib().ogbx_comm_destroy(self._h)
+            self._h = _lib.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _lib_device(device):
+    torch = _torch()
+    d = torch.device(device)
+    return torch.device('cuda', torch.cuda.current_device() if d.index is None else d.index)
+
+
+def gather_counters(counters, group=None, comm=None):
     """All-gather every rank's int64[num_tasks, 2] counters and sum them.
 
     Uses ``torch.distributed.all_gather_into_tensor`` on the default (or given)
-    process group; a no-op without an initialised group.  Returns the summed
-    counters (same device as the input) and the per-rank stack.
+    process group, or ``comm`` (an RcclComm) when given; a no-op without either.
+    Returns the summed counters (same device as the input) and the per-rank
+    stack.
     """
     torch = _torch()
     import torch.distributed as dist
 
+    if comm is not None:
+        out = comm.allgather(counters)
+        return out.sum(0), out
     if not (dist.is_available() and dist.is_initialized()):
         return counters.clone(), counters.unsqueeze(0).clone()
     world = dist.get_world_size(group)

@@ -57,3 +57,21 @@ def test_evaluate_counts_every_episode_powder(gpu):
     assert np.array_equal(t[:, 1], np.bincount(np.arange(500) % 5, minlength=5) * 3)
     assert set(metrics) == {f'evaluation/{ti["task_name"]}_success' for ti in env.task_infos} | {
         'evaluation/overall_success'}
+
+
+def test_rccl_cabi_allgather_single_rank(gpu):
+    """The C-ABI RCCL communicator (ogbx_comm_create / ogbx_eval_allgather) on
+    one rank: the gather is the identity, and gather_counters(comm=...) sums it."""
+    import torch
+
+    from ogbench_amd.evaluation import RcclComm, comm_unique_id, gather_counters
+
+    uid = comm_unique_id()
+    assert len(uid) == 128
+    comm = RcclComm(1, 0, gpu, uid)
+    c = torch.arange(10, dtype=torch.int64, device=gpu).view(5, 2) * 7 + 3
+    out = comm.allgather(c)
+    assert out.shape == (1, 5, 2) and torch.equal(out[0], c)
+    total, per_rank = gather_counters(c, comm=comm)
+    assert torch.equal(total, c) and per_rank.shape == (1, 5, 2)
+    comm.close()
