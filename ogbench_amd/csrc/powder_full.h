@@ -94,6 +94,7 @@ template <int WS, int NT>
 struct FullWorld {
   static constexpr int H = WS, W = WS, C = WS * WS, CPT = C / NT, RPK = NT / W;
   static_assert(NT % W == 0 && CPT * RPK == H, "whole rows per slab");
+  static_assert(64 % W == 0, "a wave holds whole rows (fluid row skipping)");
   PwFullShared<WS>& s;
   mutable int r0, col;
   __device__ __forceinline__ explicit FullWorld(PwFullShared<WS>& sh)
@@ -291,57 +292,63 @@ struct FullWorld {
     const bool elem = (kFluidIds >> id) & 1u;
     return match & elem & (!fdidg(a) | air) & (dens_i(a) > dens_i(sd)) & (bool)fgrav(sd) & (bool)fgrav(a);
   }
+  // Lane holding the cell (same row, column col + dc): a wave holds whole rows.
+  __device__ __forceinline__ int row_lane(int dc) const {
+    const int lane = (int)(threadIdx.x & 63u);
+    return (lane & (63 & ~(W - 1))) | ((lane + dc) & (W - 1));
+  }
+  template <typename T>
+  __device__ __forceinline__ T rowx(T x, int dc) const { return __shfl(x, row_lane(dc), 64); }
+
+  // FluidFlow (sim.py:593-667) in registers: fluid moves never leave a row and
+  // a wave holds whole rows, so each wave runs both passes on its rows with
+  // lane shuffles for the row neighbours -- no LDS staging and no barriers
+  // until the rows are written back.  real = mv & ~mv(back), real_in =
+  // real(back); the new momentum is per position.  Rows without an element
+  // that can start a move are skipped wave-uniformly.
   __device__ __forceinline__ void fluid() const {
 #ifdef OGBX_ASM_MARKS
     asm volatile("; FLUID_BEGIN");
 #endif
     fence_idx();
-    int8_t* mom2 = reinterpret_cast<int8_t*>(s.cnt);  // new momentum after pass 2
 #pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
-      const int go = pass == 0 ? -1 : 1;
-      fence_idx();
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) {
-        const int i = cell(k);
-        s.f1[i] = fluid_mv(i, nb(k, 0, go), pass, pass == 0 ? 0 : s.sw[i]);
-      }
-      sync();
-      uint32_t moved = 0;
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) {
-        const int i = cell(k), sd = nb(k, 0, go), b1 = nb(k, 0, -go), b2 = nb(k, 0, -2 * go);
-        const bool mv0 = s.f1[i], mv1 = s.f1[b1], mv2 = s.f1[b2];
-        const bool real = mv0 & !mv1, real_in = mv1 & !mv2;
-        const int nm = (pass == 0 ? 0 : s.sw[i]) + (real_in ? (pass == 0 ? 2 : -2) : 0);
-        if (pass == 0) {
-          s.f2[i] = (uint8_t)nm;  // staged: sw is read by the neighbours this pass
-        } else {
-          mom2[i] = (int8_t)nm;
-        }
-        if (real | real_in) {
-          stage_from(i, real ? sd : b1);
-          moved |= 1u << k;
-        }
-      }
-      sync();
-#pragma unroll
-      for (int k = 0; k < CPT; ++k) {
-        const int i = cell(k);
-        if ((moved >> k) & 1u) {
-          s.a[i] = s.a2[i];
-          s.m[i] = s.m2[i];
-          s.v[i] = s.v2[i];
-        }
-        if (pass == 0) s.sw[i] = (int8_t)s.f2[i];
-      }
-      sync();
-    }
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
+    for (int k = 0; k < CPT; ++k) {  // rows are independent: rolled, few live registers
       const int i = cell(k);
-      const uint32_t id = fid(s.a[i]);
-      if (is_fluid(id) || id == kKangaroo || id == kLemming) s.m[i] = mom2[i];
+      uint32_t a = s.a[i];
+      int m = s.m[i];
+      float2 v = s.v[i];
+      const uint32_t rb = s.rb[i];
+      int mom = 0;
+      if (__any((kFluidTrig >> fid(a)) & 1u)) {
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const int go = pass == 0 ? -1 : 1;
+          const uint32_t sd = rowx(a, go);
+          const uint32_t id = fid(a);
+          const int m6 = m < 0 ? 0 : (m > 0 ? 2 : 1);
+          // (rm + ch6) + mom > 0.5 for ch6 in {-2, 0, 2}, mom in {0, 2}: rand_bits
+          const bool fall = (rb >> (1 + m6 + (mom != 0 ? 3 : 0))) & 1u;
+          const bool match = pass == 0 ? fall : !fall;
+          const bool air = ((bit(kKangaroo) | bit(kLemming)) >> id) & 1u;
+          const bool elem = (kFluidIds >> id) & 1u;
+          const int mv = (int)(match & elem & (!fdidg(a) | air) & (dens_i(a) > dens_i(sd)) & (bool)fgrav(sd) &
+                               (bool)fgrav(a));
+          const int mv1 = rowx(mv, -go), mv2 = rowx(mv, -2 * go);
+          const bool real = mv & !mv1, real_in = mv1 & !mv2;
+          mom += real_in ? (pass == 0 ? 2 : -2) : 0;
+          const uint32_t ab = rowx(a, -go);
+          const int ms = rowx(m, go), mb = rowx(m, -go);
+          const float vsx = rowx(v.x, go), vsy = rowx(v.y, go), vbx = rowx(v.x, -go), vby = rowx(v.y, -go);
+          a = real ? sd : (real_in ? ab : a);
+          m = real ? ms : (real_in ? mb : m);
+          v = real ? make_float2(vsx, vsy) : (real_in ? make_float2(vbx, vby) : v);
+        }
+      }
+      const uint32_t id = fid(a);
+      if (is_fluid(id) || id == kKangaroo || id == kLemming) m = mom;
+      s.a[i] = (uint8_t)a;
+      s.m[i] = (int8_t)m;
+      s.v[i] = v;
     }
     sync();
   }
@@ -378,40 +385,67 @@ struct FullWorld {
            x == kMole || x == kLemming;
   }
 
-  // BehaviorFire (sim.py:700-790).  The 3x3 neighbourhood scans are evaluated
-  // only in the lanes whose outcome depends on them (burn candidates, cells
-  // that were fire/lava, fire that may fade, empty cells that may ignite).
+  // BehaviorFire (sim.py:700-790).  Fire and lava are sparse, so the two
+  // "is there X in my 3x3" questions are answered by dilation: the few source
+  // cells mark their 3x3 neighbourhood in a flag array (benign same-value
+  // stores) and every cell reads its own flag.  The burnable-neighbour counts
+  // are evaluated only for the cells whose outcome depends on them (cells
+  // that were fire/lava, fire that may fade, empty cells that ignite).
   __device__ __forceinline__ void fire() const {
 #ifdef OGBX_ASM_MARKS
     asm volatile("; FIRE_BEGIN");
 #endif
+    static_assert(CPT <= 4, "conversion codes packed 8 bits per cell");
     fence_idx();
-    // f1 bit 0: burns (pushes its 4 neighbours with 8), bit 1: dust near fire
-    // (pushes with 30), bit 2: fire or lava before the burn; f2: conversion
+    uint8_t* near = s.f1;  // 3x3 dilation of fire|lava before the burn
+    int8_t* hot = s.sw;    // 3x3 dilation of the cells that spread fire
+    uint32_t flb = 0;      // bit k: this cell was fire or lava before the burn
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
-      const bool fl = id == kFire || id == kLava;
-      const bool p005 = ri_lt(k, kRi005), p02 = ri_lt(k, kRi02);
-      const bool cand = (id == kWood && p005) || (id == kPlant && p02) || (id == kGas && p02) || id == kDust ||
-                        (id == kBird && p005) ||
-                        ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p02);
-      const bool cand_ice = id == kIce && p02;
-      bool near = false;
-      if (cand || cand_ice) near = box(k, [](uint32_t x) { return x == kFire || x == kLava; }) > 0;
-      const bool burn = cand && near, burn_ice = cand_ice && near;
-      s.f1[i] = (uint8_t)((burn ? 1 : 0) | (id == kDust && near ? 2 : 0) | (fl ? 4 : 0));
-      s.f2[i] = burn ? kFire + 1 : (burn_ice ? kWater + 1 : 0);
+      near[i] = 0;
+      hot[i] = 0;
+      flb |= (id == kFire || id == kLava) ? 1u << k : 0u;
     }
     sync();
 #pragma unroll
+    for (int k = 0; k < CPT; ++k)
+      if ((flb >> k) & 1u)
+#pragma unroll 1
+        for (int q = 0; q < 9; ++q) {
+          const int j = zp(k, q / 3 - 1, q % 3 - 1);
+          if (j >= 0) near[j] = 1;
+        }
+    sync();
+    // burn decisions; f2 bit 0: burns (pushes its 4 neighbours with 8), bit 1:
+    // dust near fire (pushes with 30)
+    uint32_t conv = 0;  // 8 bits per cell: new id + 1, 0 = unchanged
+#pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
-      float2 v = s.v[i];
-      // impulses away from a burning neighbour (sim.py:744-752): left, above, below, right
-      const uint32_t L = s.f1[nb(k, 0, -1)], U = s.f1[nb(k, -1, 0)], D = s.f1[nb(k, 1, 0)], R = s.f1[nb(k, 0, 1)];
-      if ((L | U | D | R) & 3u) {
+      const uint32_t id = fid(s.a[i]);
+      const bool nr = near[i];
+      const bool p005 = ri_lt(k, kRi005), p02 = ri_lt(k, kRi02);
+      const bool cand = (id == kWood && p005) | (id == kPlant && p02) | (id == kGas && p02) | (id == kDust) |
+                        (id == kBird && p005) |
+                        ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p02);
+      const bool burn = cand & nr, burn_ice = (id == kIce) & p02 & nr;
+      s.f2[i] = (uint8_t)((burn ? 1 : 0) | (((id == kDust) & nr) ? 2 : 0));
+      conv |= (burn ? kFire + 1u : (burn_ice ? kWater + 1u : 0u)) << (8 * k);
+    }
+    sync();
+    // impulses away from a burning neighbour (sim.py:744-752): left, above,
+    // below, right; then the conversions (own cells, in place)
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int i = cell(k);
+      const uint32_t L = s.f2[nb(k, 0, -1)], U = s.f2[nb(k, -1, 0)], D = s.f2[nb(k, 1, 0)], R = s.f2[nb(k, 0, 1)];
+      const uint32_t to = (conv >> (8 * k)) & 0xFFu;
+      if (to) {
+        put(i, elem(to - 1));
+      } else if ((L | U | D | R) & 3u) {
+        float2 v = s.v[i];
         v.y = v.y + 8.0f * (float)(L & 1);
         v.x = v.x + 8.0f * (float)(U & 1);
         v.x = v.x - 8.0f * (float)(D & 1);
@@ -420,58 +454,47 @@ struct FullWorld {
         v.x = v.x + 30.0f * (float)((U >> 1) & 1);
         v.x = v.x - 30.0f * (float)((D >> 1) & 1);
         v.y = v.y - 30.0f * (float)((R >> 1) & 1);
-      }
-      s.v2[i] = v;
-    }
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const uint32_t to = s.f2[i];
-      if (to) {
-        put(i, elem(to - 1));
-      } else {
-        s.v[i] = s.v2[i];
+        s.v[i] = v;
       }
     }
     sync();
-    // fire spread from (fire or lava before the burn) x burnable neighbours, and lava
+    // fire spread sources: (fire or lava before the burn) with a burnable
+    // neighbour, and lava; fading fire (no burnable neighbour)
+    uint32_t fade = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
-      const bool fl = (s.f1[i] >> 2) & 1;
+      const bool fl = (flb >> k) & 1u;
       const bool re04 = re_lt(k, kRe04);
-      const bool need = fl || (id == kFire && re04) || (id == kEmpty && re04 && ri_lt(k, kRi03));
+      const bool need = fl | ((id == kFire) & re04);
       const int nbr = need ? box(k, [](uint32_t x) { return burnable(x); }) : 1;
-      s.cnt[i] = (int16_t)((fl ? nbr : 0) + (id == kLava ? 1 : 0));
-      s.f2[i] = (uint8_t)(nbr == 0);
-    }
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const uint32_t id = fid(s.a[i]);
-      bool burn_empty = false;
-      if (id == kEmpty && ri_lt(k, kRi03)) {
-        int in_range = 0;
+      if ((fl & (nbr > 0)) | (id == kLava))
 #pragma unroll 1
         for (int q = 0; q < 9; ++q) {
           const int j = zp(k, q / 3 - 1, q % 3 - 1);
-          in_range += j >= 0 ? s.cnt[j] : 0;
+          if (j >= 0) hot[j] = 1;
         }
-        burn_empty = in_range > 0;
-      }
-      const uint32_t id2 = burn_empty ? (uint32_t)kFire : id;
-      const bool fade = id2 == kFire && re_lt(k, kRe04) && s.f2[i];
-      s.sw[i] = (int8_t)(fade ? kEmpty + 1 : (burn_empty ? kFire + 1 : 0));
+      fade |= ((id == kFire) & re04 & (nbr == 0)) ? 1u << k : 0u;
+    }
+    sync();
+    // empty cells next to a source ignite (ri < 0.3); fire with re < 0.4 and
+    // no burnable neighbour fades to empty (sim.py:778-790)
+    uint32_t conv2 = 0;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const int i = cell(k);
+      const uint32_t id = fid(s.a[i]);
+      const bool burn_empty = (id == kEmpty) & ri_lt(k, kRi03) & (hot[i] != 0);
+      bool fd = (fade >> k) & 1u;
+      if (burn_empty && re_lt(k, kRe04)) fd = box(k, [](uint32_t x) { return burnable(x); }) == 0;
+      conv2 |= (fd ? kEmpty + 1u : (burn_empty ? kFire + 1u : 0u)) << (8 * k);
     }
     sync();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const int to = s.sw[i];
-      if (to) put(i, elem((uint32_t)(to - 1)));
+      const uint32_t to = (conv2 >> (8 * k)) & 0xFFu;
+      if (to) put(cell(k), elem(to - 1));
     }
     sync();
   }
@@ -857,19 +880,16 @@ struct FullWorld {
                                          bit(kLava) | bit(kPlant) | bit(kWater);
 
   __device__ __forceinline__ void forward_masked(uint32_t P) const {
-#ifdef OGBX_PWF_RULES  // ablation builds (scripts/build_variants.sh): run only the rules in the mask
-    P &= (OGBX_PWF_RULES & 1 ? ~0u : ~bit(kStone));
-    if (!(OGBX_PWF_RULES & 4)) P &= ~(bit(kSand) | bit(kDust));
-    if (!(OGBX_PWF_RULES & 8)) P &= ~kFluidTrig;
-    if (!(OGBX_PWF_RULES & 16)) P &= ~bit(kIce);
-    if (!(OGBX_PWF_RULES & 64)) P &= ~(bit(kFire) | bit(kLava));
-    if (!(OGBX_PWF_RULES & 128)) P &= ~bit(kPlant);
-    if (!(OGBX_PWF_RULES & 256)) P &= ~kVelBit;
+#ifdef OGBX_PWF_RULES  // ablation builds (scripts/build_pwf_variants.sh): run only the rules in the mask
+    constexpr uint32_t R = OGBX_PWF_RULES;
+#else
+    constexpr uint32_t R = ~0u;
 #endif
-    if (P & bit(kStone)) stone();
+    // R bits: 1 stone, 4 sand, 8 fluid, 16 ice, 32 water, 64 fire, 128 plant, 256 velocity
+    if ((R & 1) && (P & bit(kStone))) stone();
     gravity();
-    if (P & (bit(kSand) | bit(kDust))) sand();
-    if (P & kFluidTrig) {
+    if ((R & 4) && (P & (bit(kSand) | bit(kDust)))) sand();
+    if ((R & 8) && (P & kFluidTrig)) {
       fluid();
     } else {
       // no move possible: the new momentum of every fluid cell is 0
@@ -881,16 +901,16 @@ struct FullWorld {
       sync();
     }
     if (P & bit(kIce)) {
-      ice();
+      if (R & 16) ice();
       P |= bit(kWater);
     }
-    if ((P & bit(kWater)) && (P & bit(kIce))) water();
+    if ((R & 32) && (P & bit(kWater)) && (P & bit(kIce))) water();
     if (P & (bit(kFire) | bit(kLava))) {
-      fire();
+      if (R & 64) fire();
       P |= bit(kFire) | bit(kWater) | bit(kEmpty) | kVelBit;
     }
-    if (P & bit(kPlant)) plant();
-    if (P & kVelBit) velocity();
+    if ((R & 128) && (P & bit(kPlant))) plant();
+    if ((R & 256) && (P & kVelBit)) velocity();
   }
 
 

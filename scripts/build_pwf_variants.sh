@@ -1,6 +1,6 @@
 #!/bin/bash
 # Ablation / tuning builds of the full powderworld forward (timing only; never shipped).
-# OGBX_PWF_RULES bits: 1 stone, 4 sand, 8 fluid, 16 ice(+water), 64 fire, 128 plant, 256 velocity.
+# OGBX_PWF_RULES bits: 1 stone, 4 sand, 8 fluid, 16 ice, 32 water, 64 fire, 128 plant, 256 velocity.
 # OGBX_PWF_WAVES: waves per SIMD the register budget is sized for.
 set -e
 cd "$(dirname "$0")/../ogbench_amd/csrc"
