@@ -30,6 +30,7 @@
 // fully coalesced 16-byte stores (the obs write, 24 KB per 64x64 env-step, is
 // the HBM floor of the path).
 #include <array>
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -71,6 +72,7 @@ __device__ __forceinline__ uint32_t rd(uint32_t v) { return (v & kGrav) ? (v & ~
 struct PowderParams {
   int32_t H, W, grid, brush, xy_size, num_elems, num_tasks, max_steps, tol;
   int32_t tol_task[kPwMaxTasks];  // success tolerance per task
+  float vel_q[8];                 // velocity angle-bin thresholds on q (powder_full.h, vel_bin)
   int32_t elem_ids[8];           // _elems: element id per element index
   uint32_t lut[32];              // render colour of each id, R | G<<8 | B<<16
   int32_t seq_len[kPwMaxTasks];  // goal replay sequences (elem idx, x, y)
@@ -548,6 +550,7 @@ __device__ __forceinline__ void pwf_tables(PwFullShared<WS>& sh, const PowderPar
   const int t = threadIdx.x;
   if (t < 32) sh.lut[t] = Pp->lut[t];
   if (t < 8) sh.elem_ids[t] = Pp->elem_ids[t];
+  if (t < 8) sh.vel_q[t] = Pp->vel_q[t];
   __syncthreads();
 }
 
@@ -874,6 +877,57 @@ static void full_tasks(int ne, std::vector<PwSeq>& t, std::vector<int>& tol) {
   }
 }
 
+
+// BehaviorVelocity's angle bin (sim.py:938-946) as a function of q = vy / (|v|
+// + 0.001): raw = float32(1/2pi) * float32(arccos(q)); ang = vx < 0 ? 1 - raw
+// : raw; bin = floor(ang * 8 + 0.5) mod 8, every step rounded to float32.
+// bin is a monotone step function of q on each vx branch, so it equals a
+// count of exact float32 thresholds, found here by bisection over the
+// ordered float32 values in [-1, 1]; the kernel then needs no arccos.
+static float pw_vel_raw(float q) {
+  const float inv2pi = (float)(1.0 / (2.0 * 3.141592653589793));
+  return inv2pi * (float)std::acos((double)q);
+}
+static int pw_vel_braw(float q, bool neg) {
+  const float r = pw_vel_raw(q);
+  const float ang = neg ? 1.0f - r : r;
+  return (int)std::floor(ang * 8.0f + 0.5f);
+}
+static int64_t pw_fkey(float f) {
+  uint32_t b;
+  std::memcpy(&b, &f, 4);
+  return f >= 0.0f ? (int64_t)b : -(int64_t)(b & 0x7fffffffu);
+}
+static float pw_funkey(int64_t k) {
+  const uint32_t b = (uint32_t)(k >= 0 ? k : -k);
+  float f;
+  std::memcpy(&f, &b, 4);
+  return k >= 0 ? f : -f;
+}
+// q[0..3]: vx >= 0, bin = #{k : q <= q[k-1]} (largest q with braw >= k, k = 1..4);
+// q[4..7]: vx < 0, braw = 4 + #{k : q >= q[k-1]} (smallest q with braw >= k, k = 5..8).
+static void vel_bin_thresholds(float* out) {
+  const int64_t lo0 = pw_fkey(-1.0f), hi0 = pw_fkey(1.0f);
+  for (int k = 1; k <= 4; ++k) {  // braw(q) >= k holds on [-1, T]
+    int64_t lo = lo0, hi = hi0;
+    if (pw_vel_braw(-1.0f, false) < k) { out[k - 1] = -2.0f; continue; }
+    while (lo < hi) {  // largest key with braw >= k
+      const int64_t mid = lo + (hi - lo + 1) / 2;
+      if (pw_vel_braw(pw_funkey(mid), false) >= k) lo = mid; else hi = mid - 1;
+    }
+    out[k - 1] = pw_funkey(lo);
+  }
+  for (int k = 5; k <= 8; ++k) {  // braw(q) >= k holds on [U, 1]
+    int64_t lo = lo0, hi = hi0;
+    if (pw_vel_braw(1.0f, true) < k) { out[k - 1] = 2.0f; continue; }
+    while (lo < hi) {  // smallest key with braw >= k
+      const int64_t mid = lo + (hi - lo) / 2;
+      if (pw_vel_braw(pw_funkey(mid), true) >= k) hi = mid; else lo = mid + 1;
+    }
+    out[k - 1] = pw_funkey(lo);
+  }
+}
+
 static void task_tables(int ne, std::vector<PwSeq>& t, std::vector<int>& tol) {
   if (ne == 2) {
     easy_tasks(t);
@@ -978,6 +1032,7 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
       v = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
       P.lut[i] |= (uint32_t)(uint8_t)(v * 255.0f) << (8 * c);
     }
+  vel_bin_thresholds(P.vel_q);
   std::vector<PwSeq> tasks;
   std::vector<int> tols;
   task_tables(ne, tasks, tols);

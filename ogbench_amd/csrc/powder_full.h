@@ -54,6 +54,7 @@ struct alignas(16) PwFullShared {
   };
   uint32_t lut[32];
   int32_t elem_ids[8];
+  float vel_q[8];  // angle-bin thresholds on q (PowderParams::vel_q)
   int32_t red[16];
 };
 
@@ -534,13 +535,18 @@ struct FullWorld {
     asm volatile("; VEL_BEGIN");
 #endif
     fence_idx();
-    const float inv2pi = (float)(1.0 / (2.0 * 3.141592653589793));
+#ifdef OGBX_PWF_VEL  // timing ablation: bit 0 = swap passes, bit 1 = decay + blur
+    constexpr int kVelParts = OGBX_PWF_VEL;
+#else
+    constexpr int kVelParts = 3;
+#endif
 #pragma unroll 1
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < ((kVelParts & 1) ? 2 : 0); ++pass) {
       fence_idx();
       // f2 = angle bin of cells that may move (mag above the pass threshold, not
       // wall), 0xFF otherwise; sw = chosen swap direction (-1 none)
       uint32_t dirs = 0;  // angle bins present among the cells that may move
+      uint32_t binr = 0;  // 8 bits per cell: bin, 0xFF = cannot move
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
@@ -548,16 +554,21 @@ struct FullWorld {
         const float mag = sqrtf(v.x * v.x + v.y * v.y);
         uint8_t b8 = 0xFF;
         if (mag > (pass == 0 ? 1.0f : 2.0f) && fid(s.a[i]) != kWall) {
+          // floor(8 * ang + 0.5) mod 8 with ang from float32 arccos(q): a count
+          // of exact float32 thresholds on q (host: vel_bin_thresholds)
           const float q = v.y / (mag + 0.001f);
-          const float raw = inv2pi * (float)acos((double)q);
-          const float ang = v.x < 0.0f ? 1.0f - raw : raw;
-          float b = floorf(ang * 8.0f + 0.5f);
-          b = b - 8.0f * floorf(b / 8.0f);  // np.remainder(., 8) for b >= 0
-          b8 = (uint8_t)(int)b;
+          int b;
+          if (v.x < 0.0f) {
+            b = (4 + (q >= s.vel_q[4]) + (q >= s.vel_q[5]) + (q >= s.vel_q[6]) + (q >= s.vel_q[7])) & 7;
+          } else {
+            b = (q <= s.vel_q[0]) + (q <= s.vel_q[1]) + (q <= s.vel_q[2]) + (q <= s.vel_q[3]);
+          }
+          b8 = (uint8_t)b;
           dirs |= 1u << b8;
         }
-        s.f2[i] = b8;
+        binr |= (uint32_t)b8 << (8 * k);
         s.sw[i] = -1;
+        s.f1[i] = 0;
       }
       dirs = block_or(dirs);
       if (dirs == 0) {
@@ -572,40 +583,39 @@ struct FullWorld {
         sync();
         continue;
       }
-      // swap rounds in direction order; rounds with no candidate are
-      // identities and skipped; swap choices ping-pong between sw and m2
-      int8_t* cur = s.sw;
-      int8_t* nxt = s.m2;
+      // Swap rounds in direction order (sim.py:950-962), sparse: only the
+      // cells whose bin is the round's direction test for a match (their bins
+      // live in registers); a match stamps f1 = d + 1 and, after a barrier,
+      // writes its own choice d and its target's (d + 4) mod 8 -- the
+      // target's choice wins when a matched cell is itself a target, as in
+      // the reference's where(m, a, .) then where(opp, a + 4, .).  Rounds whose
+      // bin no cell occupies are identities and skipped.
 #pragma unroll 1
       for (int d = 0; d < 8; ++d) {
         if (!((dirs >> d) & 1u)) continue;
         fence_idx();
         int dr, dc;
         dir_of(d, dr, dc);
+        uint32_t mk = 0;
 #pragma unroll
         for (int k = 0; k < CPT; ++k) {
-          const int i = cell(k), j = nb(k, dr, dc);
-          const uint32_t bi = s.f2[i], aj = s.a[j];
-          const int ci = cur[i], cj = cur[j];
-          s.f1[i] = (bi == (uint32_t)d) & (ci == -1) & (cj == -1) & (fid(aj) == kEmpty);
+          if (((binr >> (8 * k)) & 0xFFu) == (uint32_t)d) {
+            const int i = cell(k), j = nb(k, dr, dc);
+            if ((s.sw[i] == -1) & (s.sw[j] == -1) & (fid(s.a[j]) == kEmpty)) {
+              s.f1[i] = (uint8_t)(d + 1);
+              mk |= 1u << k;
+            }
+          }
         }
         sync();
 #pragma unroll
         for (int k = 0; k < CPT; ++k) {
-          const int i = cell(k);
-          int8_t w = cur[i];
-          if (s.f1[i]) w = (int8_t)d;
-          if (s.f1[nb(k, -dr, -dc)]) w = (int8_t)((d + 4) & 7);
-          nxt[i] = w;
+          if ((mk >> k) & 1u) {
+            const int i = cell(k);
+            s.sw[nb(k, dr, dc)] = (int8_t)((d + 4) & 7);
+            if (s.f1[nb(k, -dr, -dc)] != (uint8_t)(d + 1)) s.sw[i] = (int8_t)d;
+          }
         }
-        sync();
-        int8_t* t = cur;
-        cur = nxt;
-        nxt = t;
-      }
-      if (cur != s.sw) {
-#pragma unroll
-        for (int k = 0; k < CPT; ++k) s.sw[cell(k)] = cur[cell(k)];
         sync();
       }
       uint32_t moved = 0;
@@ -630,16 +640,9 @@ struct FullWorld {
         s.v[i] = v;
       });
     }
-    // decay and 3x3 blur (zero padded), NumPy's einsum summation order
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      float2 v = s.v[i];
-      v.x = v.x * 0.95f;
-      v.y = v.y * 0.95f;
-      s.v[i] = v;
-    }
-    sync();
+    // decay (x0.95) fused into the 3x3 blur (zero padded) of the decayed
+    // field, NumPy's einsum summation order
+    if (!(kVelParts & 2)) return;
     const float w18 = 1.0f / 18.0f;
     fence_idx();
 #pragma unroll
@@ -649,10 +652,12 @@ struct FullWorld {
       for (int q = 0; q < 9; ++q) {
         const int j = zp(k, q / 3 - 1, q % 3 - 1);
         const float2 v = j >= 0 ? s.v[j] : make_float2(0.f, 0.f);
-        tx[q] = v.x * w18;
-        ty[q] = v.y * w18;
+        tx[q] = (v.x * 0.95f) * w18;
+        ty[q] = (v.y * 0.95f) * w18;
       }
-      const float2 own = s.v[cell(k)];
+      float2 own = s.v[cell(k)];
+      own.x = own.x * 0.95f;
+      own.y = own.y * 0.95f;
       const float bx = (((tx[4] + tx[0]) + tx[8]) + (tx[5] + tx[1])) + ((tx[6] + tx[2]) + (tx[7] + tx[3]));
       const float by = (((ty[4] + ty[0]) + ty[8]) + (ty[5] + ty[1])) + ((ty[6] + ty[2]) + (ty[7] + ty[3]));
       s.v2[cell(k)] = make_float2(bx + own.x * 0.5f, by + own.y * 0.5f);
