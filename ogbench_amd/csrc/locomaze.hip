@@ -69,6 +69,15 @@ namespace ogbx {
 
 // ------------------------------------------------------------ device helpers
 
+// The contact model is the same for every maze (P.pm == kPointModel, checked at
+// create): the step kernels use the compile-time copy so its ~30 constants fold
+// into the instructions instead of living in (spilled) SGPRs.
+#ifdef OGBX_RUNTIME_MODEL
+#define OGBX_POINT_MODEL(pm, P) const PointModel pm = (P).pm
+#else
+#define OGBX_POINT_MODEL(pm, P) constexpr PointModel pm = kPointModel
+#endif
+
 __device__ inline void stage_wall(const MazeParams& P, uint8_t* wall_s) {
   for (int t = threadIdx.x; t < P.H * P.W; t += blockDim.x) wall_s[t] = P.wall[t];
   __syncthreads();
@@ -198,7 +207,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     uint8_t* __restrict__ truncated, uint8_t* __restrict__ success,
     double* __restrict__ final_obs, int32_t auto_reset, uint32_t k0, uint32_t k1, int epw) {
   const MazeParams& P = *Pp;
-  const PointModel pm = P.pm;
+  OGBX_POINT_MODEL(pm, P);
   __shared__ uint16_t nb_s[kMaxCells];
   stage_nbmask(P, nb_s);
   const int64_t i = env_of_lane(epw);
@@ -277,7 +286,7 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
                                                             double* qpos_out,
                                                             uint8_t* contact_out, int epw) {
   const MazeParams& P = *Pp;
-  const PointModel pm = P.pm;
+  OGBX_POINT_MODEL(pm, P);
   __shared__ uint16_t nb_s[kMaxCells];
   stage_nbmask(P, nb_s);
   const int64_t i = env_of_lane(epw);
@@ -563,7 +572,7 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
   e->n = n_envs;
   MazeParams& P = e->P;
   std::memset(&P, 0, sizeof(P));
-  P.pm = make_point_model(4.0, 4.0);
+  P.pm = kPointModel;
   P.H = spec->H;
   P.W = spec->W;
   P.num_tasks = spec->ntasks;
@@ -669,11 +678,11 @@ ogbx_status ogbx_diag_phys_stamps(unsigned long long* out) {
 #endif
 
 #ifdef OGBX_PHYS_STATS
-// Diagnostic build only: read and clear the physics path counters.
-ogbx_status ogbx_diag_phys_stats(unsigned long long* out8) {
+// Diagnostic build only: read and clear the 16 physics path counters.
+ogbx_status ogbx_diag_phys_stats(unsigned long long* out16) {
   OGBX_HIP(hipDeviceSynchronize());
-  OGBX_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_phys_stats), 8 * sizeof(unsigned long long)));
-  unsigned long long z[8] = {0};
+  OGBX_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phys_stats), 16 * sizeof(unsigned long long)));
+  unsigned long long z[16] = {0};
   OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phys_stats), z, sizeof(z)));
   return OGBX_OK;
 }

@@ -63,6 +63,16 @@ struct PointModel {
 
 constexpr double kMinVal = 1e-15;  // mjMINVAL
 
+// 1/d for d > 0 in the normal range: v_rcp_f64 + two Newton-Raphson
+// refinements (5 dependent instructions instead of the 10 of the IEEE
+// division sequence; within an ulp of the quotient).
+__device__ __forceinline__ double fast_recip(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return r;
+}
+
 #ifdef OGBX_PHYS_STAMPS
 // Diagnostic build only: per-wave cycle sums of the stage-loop segments
 // [collide, solve, update, whole point_step], indexed by global wave id.
@@ -90,10 +100,16 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 #ifdef OGBX_PHYS_STATS
 // Diagnostic build only (-DOGBX_PHYS_STATS): per-path counters.
-__device__ unsigned long long g_phys_stats[8];
+__device__ unsigned long long g_phys_stats[16];
 #define OGBX_STAT(k) atomicAdd(&g_phys_stats[k], 1ull)
+// once per wave when any active lane satisfies cond
+#define OGBX_WSTAT(k, cond) do {                                                   \
+    const unsigned long long _b = __ballot(1);                                     \
+    if (__any(cond) && (int)(threadIdx.x & 63) == __ffsll((long long)_b) - 1)      \
+      atomicAdd(&g_phys_stats[k], 1ull); } while (0)
 #else
 #define OGBX_STAT(k) ((void)0)
+#define OGBX_WSTAT(k, cond) ((void)0)
 #endif
 
 // A sphere whose centre lies in an empty cell touches at most 3 wall boxes
@@ -145,6 +161,17 @@ __device__ __forceinline__ void contact_gains(const PointModel& pm, double dist,
   }
 }
 
+// Clamp of a box-frame coordinate to [-h, h] (the closest point of the box).
+// v_max/v_min_f64: two instructions instead of two compares and four selects;
+// identical results (signed zeros inside the range pass through unchanged).
+__device__ __forceinline__ double clamp_box(double p, double h) {
+#ifdef OGBX_CLAMP_SELECT
+  return p < -h ? -h : (p > h ? h : p);
+#else
+  return __builtin_fmin(__builtin_fmax(p, -h), h);
+#endif
+}
+
 // Store one contact into slot `slot` (runtime index, per-field selects: a
 // branchy store would be merged by SimplifyCFG into one store through a
 // selected address -> scratch).
@@ -194,9 +221,9 @@ __device__ __forceinline__ int collide_walls_generic(const PointModel& pm, const
     const double px = x - (cx + dj * u);
     const double py = y - (cy + di * u);
     const double pz = pm.sphere_z - pm.box_cz;
-    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
-    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
-    const double clz = pz < -hz ? -hz : (pz > hz ? hz : pz);
+    const double clx = clamp_box(px, hx);
+    const double cly = clamp_box(py, hx);
+    const double clz = clamp_box(pz, hz);
     const double tx = clx - px, ty = cly - py, tz = clz - pz;
     const double d2 = tx * tx + ty * ty + tz * tz;
     if (d2 > pm.r2_hi || nc >= kMaxContacts) continue;  // certainly d - r > 0
@@ -271,18 +298,44 @@ __device__ __forceinline__ int collide_walls_generic(const PointModel& pm, const
 // contact are all-zero (their rows are inactive in every solver).
 // Rare geometry (centre in a wall cell / off the map / exactly on a face) is
 // routed to collide_walls_generic.
-__device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_t* nbmask, int H,
-                                             int W, double x, double y, Contacts& c) {
-  const double fi = floor((y + pm.off_y + 0.5 * pm.unit) * pm.inv_unit);
-  const double fj = floor((x + pm.off_x + 0.5 * pm.unit) * pm.inv_unit);
-  const double cx = fj * pm.unit - pm.off_x, cy = fi * pm.unit - pm.off_y;
+// The cell of the sphere centre and its 3x3 wall mask.  A step moves the
+// centre by far less than a cell, so point_step computes this once per step and
+// again only when the centre leaves the inner part of the cell (cell_frame_valid).
+struct CellFrame {
+  double fi, fj, cx, cy;  // cell indices (as doubles) and cell centre
+  uint32_t m;             // 3x3 neighbourhood wall mask (0x1FF off the map)
+  bool inside;            // cell within the map
+};
+
+__device__ __forceinline__ void cell_frame(const PointModel& pm, const uint16_t* nbmask, int H, int W,
+                                           double x, double y, CellFrame& f) {
+  f.fi = floor((y + pm.off_y + 0.5 * pm.unit) * pm.inv_unit);
+  f.fj = floor((x + pm.off_x + 0.5 * pm.unit) * pm.inv_unit);
+  f.cx = f.fj * pm.unit - pm.off_x;
+  f.cy = f.fi * pm.unit - pm.off_y;
+  f.inside = f.fi >= 0.0 && f.fi < (double)H && f.fj >= 0.0 && f.fj < (double)W;
+  f.m = f.inside ? nbmask[(int)f.fi * W + (int)f.fj] : 0x1FFu;
+}
+
+// True when (x, y) is certainly still in the frame's cell: |offset| < 0.49975
+// unit puts (x + off + unit/2) / unit strictly inside (fj, fj + 1), so the
+// floor() of cell_frame would return the same cell.
+__device__ __forceinline__ bool cell_frame_valid(const PointModel& pm, const CellFrame& f, double x,
+                                                 double y) {
+  const double lim = 0.49975 * pm.unit;
+  return fabs(x - f.cx) < lim && fabs(y - f.cy) < lim;
+}
+
+__device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint16_t* nbmask, int H,
+                                                int W, double x, double y, const CellFrame& f,
+                                                Contacts& c) {
+  const double fi = f.fi, fj = f.fj, cx = f.cx, cy = f.cy;
+  const uint32_t m = f.m;
   const double lx = x - cx, ly = y - cy;  // offset from own cell centre
   const double reach = pm.box_hxy - pm.radius - 1e-9;
   const int sx = lx >= reach ? 1 : (lx <= -reach ? -1 : 0);
   const int sy = ly >= reach ? 1 : (ly <= -reach ? -1 : 0);
-  const bool inside = fi >= 0.0 && fi < (double)H && fj >= 0.0 && fj < (double)W;
-  const uint32_t m = inside ? nbmask[(int)fi * W + (int)fj] : 0x1FFu;
-  bool slow = !inside || ((m >> 4) & 1u);
+  bool slow = !f.inside || ((m >> 4) & 1u);
   const double hx = pm.box_hxy, r = pm.radius, u = pm.unit;
   // role validity from the neighbourhood mask
   const bool vX = sx != 0 && ((m >> (4 + sx)) & 1u);
@@ -292,8 +345,8 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
   double dX, tXx, tXy;
   {
     const double px = x - (cx + sx * u), py = y - cy;
-    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
-    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    const double clx = clamp_box(px, hx);
+    const double cly = clamp_box(py, hx);
     tXx = clx - px;
     tXy = cly - py;
     dX = fabs(tXx);
@@ -301,8 +354,8 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
   double dY, tYx, tYy;
   {
     const double px = x - cx, py = y - (cy + sy * u);
-    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
-    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    const double clx = clamp_box(px, hx);
+    const double cly = clamp_box(py, hx);
     tYx = clx - px;
     tYy = cly - py;
     dY = fabs(tYy);
@@ -310,8 +363,8 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
   double tDx, tDy, d2D;
   {
     const double px = x - (cx + sx * u), py = y - (cy + sy * u);
-    const double clx = px < -hx ? -hx : (px > hx ? hx : px);
-    const double cly = py < -hx ? -hx : (py > hx ? hx : py);
+    const double clx = clamp_box(px, hx);
+    const double cly = clamp_box(py, hx);
     tDx = clx - px;
     tDy = cly - py;
     d2D = tDx * tDx + tDy * tDy;
@@ -322,6 +375,8 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
   // exact-geometry guards: face roles must really be faces, d > mjMINVAL
   slow = slow || (cX && (tXy != 0.0 || dX <= kMinVal)) || (cY && (tYx != 0.0 || dY <= kMinVal));
   double dD = 0.0, nDx = 0.0, nDy = 0.0;
+  OGBX_WSTAT(11, cD);
+  OGBX_WSTAT(12, slow);
   if (cD && !slow) {  // vertical-edge contact of the diagonal box
     dD = sqrt(d2D);
     if (dD - r > 0.0) {
@@ -329,7 +384,7 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
     } else if (dD <= kMinVal) {
       slow = true;
     } else {
-      const double inv = 1.0 / dD;
+      const double inv = fast_recip(dD);
       nDx = -tDx * inv;
       nDy = -tDy * inv;
     }
@@ -337,6 +392,8 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
 #ifndef OGBX_MICRO_NO_GENERIC
   if (__builtin_expect(slow, 0)) return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
 #endif
+  OGBX_WSTAT(10, (cX && fabs(dX - r) * pm.inv_width < 1.0) || (cY && fabs(dY - r) * pm.inv_width < 1.0) ||
+                     (cD && fabs(dD - r) * pm.inv_width < 1.0));
   double D, kp;
   // s0: x face, n = (-sign(tx), -ty) with ty = +-0
   contact_gains(pm, dX - r, &D, &kp);
@@ -364,6 +421,13 @@ __device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_
   c.s2.w = cD ? D : 0.0;
   c.n = (int)cX + (int)cY + (int)cD;
   return c.n;
+}
+
+__device__ __forceinline__ int collide_walls(const PointModel& pm, const uint16_t* nbmask, int H,
+                                             int W, double x, double y, Contacts& c) {
+  CellFrame f;
+  cell_frame(pm, nbmask, H, W, x, y, f);
+  return collide_in_frame(pm, nbmask, H, W, x, y, f, c);
 }
 
 // ---------------------------------------------------------------------------
@@ -519,11 +583,12 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
 #pragma unroll 1
   for (int it = 0; it < 8; ++it) {
     OGBX_STAT(4);
+    OGBX_WSTAT(13, true);
     if (g[0] == 0.0 && g[1] == 0.0) {
       done = true;
       break;
     }
-    const double idet = 1.0 / (h[0] * h[2] - h[1] * h[1]);
+    const double idet = fast_recip(h[0] * h[2] - h[1] * h[1]);  // det >= M^2 > 0
     ux -= (h[2] * g[0] - h[1] * g[1]) * idet;
     uy -= (h[0] * g[1] - h[1] * g[0]) * idet;
     if (active_set(c, live, ux, uy) == act) {
@@ -574,6 +639,8 @@ __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& 
   double ux = cux, uy = cuy;
   OGBX_STAT(c.n);
   bool need_newton;
+  OGBX_WSTAT(9, true);
+  OGBX_WSTAT(8, c.n >= 2);
   if (__any(c.n >= 2)) {
     need_newton = c.n >= 1;
     ux = c.n >= 1 ? *wx : cux;
@@ -605,8 +672,10 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
                                  double* px, double* py) {
   double x = *px, y = *py;
   Contacts c;
+  CellFrame fr;
   OGBX_STAMP_DECL
-  if (collide_walls(pm, wall, H, W, x, y, c) == 0) {
+  cell_frame(pm, wall, H, W, x, y, fr);
+  if (collide_in_frame(pm, wall, H, W, x, y, fr, c) == 0) {
     *px = x + 0.0;
     *py = y + 0.0;
     OGBX_STAMP_END;
@@ -628,7 +697,10 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
     const int st = e & 3;
     double fx, fy;
 #ifndef OGBX_ABLATE_COLLIDE
-    if (e != 0) collide_walls(pm, wall, H, W, qsx, qsy, c);
+    if (e != 0) {
+      if (__builtin_expect(!cell_frame_valid(pm, fr, qsx, qsy), 0)) cell_frame(pm, wall, H, W, qsx, qsy, fr);
+      collide_in_frame(pm, wall, H, W, qsx, qsy, fr, c);
+    }
 #endif
     OGBX_STAMP_SEG(_ta);
     solve_acc(pm, c, vsx, vsy, &fx, &fy, &wux, &wuy);
@@ -667,9 +739,10 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
   return 1;
 }
 
-// Host-side constants of the model (shared by libogbx and the microbenchmarks).
 // MuJoCo-derived constants of the point model (DESIGN.md lists each source).
-inline PointModel make_point_model(double unit, double off) {
+// constexpr: every locomaze maze uses maze_unit = 4 and offset 4, so the
+// kernels fold kPointModel into immediates instead of reading it per launch.
+constexpr PointModel make_point_model(double unit, double off) {
   PointModel pm{};
   const double pi = 3.14159265358979323846;
   const double r = 0.7, density = 100.0;
@@ -677,15 +750,14 @@ inline PointModel make_point_model(double unit, double off) {
   pm.h = 0.02;
   pm.nsub = 5;
   // solref (0.02, 1) with refsafe: timeconst = max(0.02, 2*dt) = 0.04
-  const double timeconst = std::fmax(0.02, 2.0 * pm.h), dampratio = 1.0;
-  // solimp (0.9, 0.95, 0.001, 0.5, 2)
+  const double timeconst = 0.02 > 2.0 * pm.h ? 0.02 : 2.0 * pm.h, dampratio = 1.0;
+  // solimp (0.9, 0.95, 0.001, 0.5, 2); power 2: a = 1/mid^(p-1), b = 1/(1-mid)^(p-1)
   pm.imp_dmin = 0.9;
   pm.imp_dmax = 0.95;
   pm.imp_width = 0.001;
   pm.imp_mid = 0.5;
-  const double power = 2.0;
-  pm.imp_a = 1.0 / std::pow(pm.imp_mid, power - 1.0);
-  pm.imp_b = 1.0 / std::pow(1.0 - pm.imp_mid, power - 1.0);
+  pm.imp_a = 1.0 / pm.imp_mid;
+  pm.imp_b = 1.0 / (1.0 - pm.imp_mid);
   const double dmax = pm.imp_dmax;
   pm.K = 1.0 / (dmax * dmax * timeconst * timeconst * dampratio * dampratio);
   pm.B = 2.0 / (dmax * timeconst);
@@ -723,5 +795,8 @@ inline PointModel make_point_model(double unit, double off) {
   pm.inv_width = 1.0 / pm.imp_width;
   return pm;
 }
+
+// The model of every locomaze maze (maze_unit 4, offset 4: maze.py:83-86).
+constexpr PointModel kPointModel = make_point_model(4.0, 4.0);
 
 }  // namespace ogbx
