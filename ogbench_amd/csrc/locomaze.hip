@@ -17,6 +17,7 @@
 //   xy_to_ij / ij_to_xy / add_noise  maze.py:552-567
 //   PointEnv.step   ogbench/locomaze/point.py:64-95
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -63,6 +64,7 @@ struct ogbx_maze_env {
   uint64_t seed = 0;
   bool was_reset = false;
   int epw = 64;  // envs per 64-lane wave of the step/physics kernels
+  int lds_pad = 0;  // dynamic LDS bytes requested per step/physics workgroup
 };
 
 namespace ogbx {
@@ -569,6 +571,13 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
 
   auto* e = new ogbx_maze_env();
   e->device = device;
+  if (const char* v = std::getenv("OGBX_MAZE_LDS")) {  // diagnostic placement knob (A/B only)
+    e->lds_pad = std::atoi(v);
+    hipFuncSetAttribute((const void*)maze_step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    hipFuncSetAttribute((const void*)maze_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    hipFuncSetAttribute((const void*)point_physics_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    hipFuncSetAttribute((const void*)point_physics_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+  }
   e->n = n_envs;
   MazeParams& P = e->P;
   std::memset(&P, 0, sizeof(P));
@@ -761,11 +770,11 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
   const int epw = e->epw;
   dim3 grid(grid_for(e->n * (64 / epw), 256)), block(256);
   if (action_is_f64)
-    hipLaunchKernelGGL(maze_step_kernel<true>, grid, block, 0, (hipStream_t)stream, e->Pd, e->S,
+    hipLaunchKernelGGL(maze_step_kernel<true>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
                        final_obs, auto_reset, k0, k1, epw);
   else
-    hipLaunchKernelGGL(maze_step_kernel<false>, grid, block, 0, (hipStream_t)stream, e->Pd, e->S,
+    hipLaunchKernelGGL(maze_step_kernel<false>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
                        final_obs, auto_reset, k0, k1, epw);
   OGBX_LAUNCHED("maze_step_kernel");
@@ -794,10 +803,10 @@ ogbx_status ogbx_point_physics(ogbx_maze_t e, const double* qpos_in, const void*
   const int epw = e->epw;
   dim3 grid(grid_for(n * (64 / epw), 256)), block(256);
   if (action_is_f64)
-    hipLaunchKernelGGL(point_physics_kernel<true>, grid, block, 0, (hipStream_t)stream, e->Pd,
+    hipLaunchKernelGGL(point_physics_kernel<true>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd,
                        qpos_in, action, n, qpos_out, contact_out, epw);
   else
-    hipLaunchKernelGGL(point_physics_kernel<false>, grid, block, 0, (hipStream_t)stream, e->Pd,
+    hipLaunchKernelGGL(point_physics_kernel<false>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd,
                        qpos_in, action, n, qpos_out, contact_out, epw);
   OGBX_LAUNCHED("point_physics_kernel");
   return OGBX_OK;

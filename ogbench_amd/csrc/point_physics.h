@@ -377,6 +377,18 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
   double dD = 0.0, nDx = 0.0, nDy = 0.0;
   OGBX_WSTAT(11, cD);
   OGBX_WSTAT(12, slow);
+#ifndef OGBX_DIAG_BRANCHY
+  {  // vertical-edge contact of the diagonal box, straight-line (no divergent branch)
+    const double dd = sqrt(cD ? d2D : 1.0);
+    const double inv = fast_recip(dd);
+    const bool far = dd - r > 0.0;
+    slow = slow || (cD && !far && dd <= kMinVal);
+    cD = cD && !far;
+    dD = cD ? dd : 0.0;
+    nDx = cD ? -tDx * inv : 0.0;
+    nDy = cD ? -tDy * inv : 0.0;
+  }
+#else
   if (cD && !slow) {  // vertical-edge contact of the diagonal box
     dD = sqrt(d2D);
     if (dD - r > 0.0) {
@@ -389,6 +401,7 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
       nDy = -tDy * inv;
     }
   }
+#endif
 #ifndef OGBX_MICRO_NO_GENERIC
   if (__builtin_expect(slow, 0)) return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
 #endif
@@ -452,6 +465,15 @@ __device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Co
   const double cn = nx * cux + ny * cuy, ct = tx * cux + ty * cuy;
   double un = cn, ut = ct;
   bool ok = true;
+#ifndef OGBX_ONE_BRANCHY
+  const bool empty_ok = cn + e + ct >= 0.0 && cn + e - ct >= 0.0;  // {} is consistent
+  {  // straight-line: every candidate is evaluated, the selects pick one
+    const double a11 = M + 3.0 * w, a22 = M + w;
+    const bool wmax = w == pm.w_max;
+    const double i2 = wmax ? pm.inv_M2w : fast_recip(M + 2.0 * w);
+    const double i4 = wmax ? pm.inv_M4w : fast_recip(M + 4.0 * w);
+    const double idet = wmax ? pm.inv_det3 : fast_recip(a11 * a22 - w * w);
+#else
   if (!(cn + e + ct >= 0.0 && cn + e - ct >= 0.0)) {  // {} is not consistent
     double i2, i4, idet;
     const double a11 = M + 3.0 * w, a22 = M + w;
@@ -464,6 +486,7 @@ __device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Co
       i4 = 1.0 / (M + 4.0 * w);
       idet = 1.0 / (a11 * a22 - w * w);
     }
+#endif
     // {+}: rank-1 update along J = n + t (|J|^2 = 2)
     const double rp = cn + e + ct;
     const double bpn = cn - w * rp * i2, bpt = ct - w * rp * i2;
@@ -495,6 +518,11 @@ __device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Co
     un = kP ? bpn : un;
     ut = kP ? bpt : ut;
     ok = kP || kM || kDP || kDM || kF;
+#ifndef OGBX_ONE_BRANCHY
+    un = empty_ok ? cn : un;
+    ut = empty_ok ? ct : ut;
+    ok = ok || empty_ok;
+#endif
   }
   *ux = un * nx + ut * tx;
   *uy = un * ny + ut * ty;
@@ -580,8 +608,33 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
   double g[2], h[3], f;
   bool done = false;
   uint32_t act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
+#ifndef OGBX_NEWTON_LOOP_ONLY
+  {  // OGBX_NEWTON_NFIX unconditional full steps (straight-line, no per-lane
+     // exits); converged if the active set after the last step is the piece
+     // it minimised
+#ifndef OGBX_NEWTON_NFIX
+#define OGBX_NEWTON_NFIX 2
+#endif
+    double idet;
+#pragma unroll
+    for (int it = 1; it < OGBX_NEWTON_NFIX; ++it) {
+      idet = fast_recip(h[0] * h[2] - h[1] * h[1]);
+      ux -= (h[2] * g[0] - h[1] * g[1]) * idet;
+      uy -= (h[0] * g[1] - h[1] * g[0]) * idet;
+      act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
+    }
+    idet = fast_recip(h[0] * h[2] - h[1] * h[1]);
+    const double vx = ux - (h[2] * g[0] - h[1] * g[1]) * idet;
+    const double vy = uy - (h[0] * g[1] - h[1] * g[0]) * idet;
+    const bool conv = (g[0] == 0.0 && g[1] == 0.0) || active_set(c, live, vx, vy) == act;
+    ux = (g[0] == 0.0 && g[1] == 0.0) ? ux : vx;
+    uy = (g[0] == 0.0 && g[1] == 0.0) ? uy : vy;
+    done = conv;
+    if (__any(!done)) act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
+  }
+#endif
 #pragma unroll 1
-  for (int it = 0; it < 8; ++it) {
+  for (int it = 0; it < 8 && !done; ++it) {
     OGBX_STAT(4);
     OGBX_WSTAT(13, true);
     if (g[0] == 0.0 && g[1] == 0.0) {
