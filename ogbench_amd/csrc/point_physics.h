@@ -129,6 +129,7 @@ struct ContactSlot {
 // into a dynamically indexed store, so the contacts never leave VGPRs.
 struct Contacts {
   int n;
+  bool roles;  // slots hold the role layout of collide_in_frame (s0 x face, s1 y face)
   ContactSlot s0, s1, s2;
 };
 
@@ -283,6 +284,7 @@ __device__ __forceinline__ int collide_walls_generic(const PointModel& pm, const
     }
   }
   c.n = nc;
+  c.roles = false;
   return nc;
 }
 
@@ -433,6 +435,7 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
   c.s2.kp = cD ? kp : 0.0;
   c.s2.w = cD ? D : 0.0;
   c.n = (int)cX + (int)cY + (int)cD;
+  c.roles = true;
   return c.n;
 }
 
@@ -533,7 +536,32 @@ __device__ __forceinline__ bool solve_one_contact(const PointModel& pm, const Co
 // active-edge mask.  `live` has bit s set when some lane of the wave holds a
 // contact in slot s (wave-uniform): empty slots are all-zero rows (r = 0,
 // never active), so skipping a slot no lane uses changes nothing.
-template <bool kWithF>
+// Role layout (kRoles): s0 is an x face, n = (s, +-0), t = (+-0, s), and s1 a
+// y face, n = (+-0, q), t = (-q, +-0), with s, q in {-1, 0, 1} (0 = no
+// contact, w = 0).  Their rows n+t, n-t, n then have entries in {-1, 0, 1}, so
+// a, b and the residuals are the generic ones exactly, and the gradient /
+// Hessian contributions collapse to sums of the weighted residuals:
+//   s0: g += s*(q0+q1+q2, q0-q1),  h += (W0+W1+W2, W0-W1, W0+W1)
+//   s1: g += q*(q1-q0, q0+q1+q2),  h += (W0+W1, W1-W0, W0+W1+W2)
+// (q_e = W_e r_e, W_e the active weights; only the summation order differs).
+template <bool kRoles>
+__device__ __forceinline__ void slot_ab(const Contacts& c, int s, double ux, double uy, double* a,
+                                        double* b) {
+#pragma clang fp contract(fast)
+  const ContactSlot& k = slot_of(c, s);
+  if (kRoles && s == 0) {
+    *a = k.nx * ux + k.kp;
+    *b = k.nx * uy;
+  } else if (kRoles && s == 1) {
+    *a = k.ny * uy + k.kp;
+    *b = -(k.ny * ux);
+  } else {
+    *a = k.nx * ux + k.ny * uy + k.kp;
+    *b = k.tx * ux + k.ty * uy;
+  }
+}
+
+template <bool kWithF, bool kRoles = false>
 __device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Contacts& c, uint32_t live,
                                                double cux, double cuy, double ux, double uy, double* g,
                                                double* h, double* fval) {
@@ -549,8 +577,30 @@ __device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Conta
   for (int s = 0; s < kMaxContacts; ++s) {
     if (live & (1u << s)) {
       const ContactSlot& k = slot_of(c, s);
-      const double a = k.nx * ux + k.ny * uy + k.kp;
-      const double b = k.tx * ux + k.ty * uy;
+      double a, b;
+      slot_ab<kRoles>(c, s, ux, uy, &a, &b);
+      if (kRoles && !kWithF && s < 2) {
+        const double r0 = a + b, r1 = a - b, r2 = a;
+        const bool o0 = r0 < 0.0, o1 = r1 < 0.0, o2 = r2 < 0.0;
+        const double W0 = o0 ? k.w : 0.0, W1 = o1 ? k.w : 0.0, W2 = o2 ? 2.0 * k.w : 0.0;
+        act |= ((o0 ? 1u : 0u) | (o1 ? 2u : 0u) | (o2 ? 4u : 0u)) << (3 * s);
+        const double q0 = W0 * r0, q1 = W1 * r1, q2 = W2 * r2;
+        const double qs = q0 + q1 + q2, W01 = W0 + W1;
+        if (s == 0) {
+          g[0] += k.nx * qs;
+          g[1] += k.nx * (q0 - q1);
+          h[0] += W01 + W2;
+          h[1] += W0 - W1;
+          h[2] += W01;
+        } else {
+          g[0] += k.ny * (q1 - q0);
+          g[1] += k.ny * qs;
+          h[0] += W01;
+          h[1] += W1 - W0;
+          h[2] += W01 + W2;
+        }
+        continue;
+      }
 #pragma unroll
       for (int e = 0; e < 3; ++e) {
         const double sg = e == 0 ? 1.0 : (e == 1 ? -1.0 : 0.0);
@@ -576,15 +626,15 @@ __device__ __forceinline__ uint32_t eval_piece(const PointModel& pm, const Conta
 }
 
 // Active-edge mask at u only (no derivatives).
+template <bool kRoles = false>
 __device__ __forceinline__ uint32_t active_set(const Contacts& c, uint32_t live, double ux, double uy) {
 #pragma clang fp contract(fast)
   uint32_t act = 0;
 #pragma unroll
   for (int s = 0; s < kMaxContacts; ++s) {
     if (live & (1u << s)) {
-      const ContactSlot& k = slot_of(c, s);
-      const double a = k.nx * ux + k.ny * uy + k.kp;
-      const double b = k.tx * ux + k.ty * uy;
+      double a, b;
+      slot_ab<kRoles>(c, s, ux, uy, &a, &b);
       act |= (a + b < 0.0 ? 1u : 0u) << (3 * s);
       act |= (a - b < 0.0 ? 1u : 0u) << (3 * s + 1);
       act |= (a < 0.0 ? 1u : 0u) << (3 * s + 2);
@@ -601,13 +651,14 @@ __device__ __forceinline__ uint32_t active_set(const Contacts& c, uint32_t live,
 // derivative evaluation + one mask evaluation per converged stage).  Safety
 // net: damped Newton with Armijo backtracking from cu (monotone, globally
 // convergent).
+template <bool kRoles>
 __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contacts& c, uint32_t live,
                                              double cux, double cuy, double* ux_io, double* uy_io) {
 #pragma clang fp contract(fast)
   double ux = *ux_io, uy = *uy_io;
   double g[2], h[3], f;
   bool done = false;
-  uint32_t act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
+  uint32_t act = eval_piece<false, kRoles>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
 #ifndef OGBX_NEWTON_LOOP_ONLY
   {  // OGBX_NEWTON_NFIX unconditional full steps (straight-line, no per-lane
      // exits); converged if the active set after the last step is the piece
@@ -621,16 +672,16 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
       idet = fast_recip(h[0] * h[2] - h[1] * h[1]);
       ux -= (h[2] * g[0] - h[1] * g[1]) * idet;
       uy -= (h[0] * g[1] - h[1] * g[0]) * idet;
-      act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
+      act = eval_piece<false, kRoles>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
     }
     idet = fast_recip(h[0] * h[2] - h[1] * h[1]);
     const double vx = ux - (h[2] * g[0] - h[1] * g[1]) * idet;
     const double vy = uy - (h[0] * g[1] - h[1] * g[0]) * idet;
-    const bool conv = (g[0] == 0.0 && g[1] == 0.0) || active_set(c, live, vx, vy) == act;
+    const bool conv = (g[0] == 0.0 && g[1] == 0.0) || active_set<kRoles>(c, live, vx, vy) == act;
     ux = (g[0] == 0.0 && g[1] == 0.0) ? ux : vx;
     uy = (g[0] == 0.0 && g[1] == 0.0) ? uy : vy;
     done = conv;
-    if (__any(!done)) act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
+    if (__any(!done)) act = eval_piece<false, kRoles>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
   }
 #endif
 #pragma unroll 1
@@ -644,11 +695,11 @@ __device__ __forceinline__ void solve_newton(const PointModel& pm, const Contact
     const double idet = fast_recip(h[0] * h[2] - h[1] * h[1]);  // det >= M^2 > 0
     ux -= (h[2] * g[0] - h[1] * g[1]) * idet;
     uy -= (h[0] * g[1] - h[1] * g[0]) * idet;
-    if (active_set(c, live, ux, uy) == act) {
+    if (active_set<kRoles>(c, live, ux, uy) == act) {
       done = true;
       break;
     }
-    act = eval_piece<false>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
+    act = eval_piece<false, kRoles>(pm, c, live, cux, cuy, ux, uy, g, h, &f);
   }
   if (!done) {
     OGBX_STAT(5);
@@ -708,7 +759,12 @@ __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& 
   if (need_newton) {
     const uint32_t live = (__any(c.s0.w != 0.0) ? 1u : 0u) | (__any(c.s1.w != 0.0) ? 2u : 0u) |
                           (__any(c.s2.w != 0.0) ? 4u : 0u);
-    solve_newton(pm, c, live, cux, cuy, &ux, &uy);
+#ifdef OGBX_NO_ROLE_EVAL
+    solve_newton<false>(pm, c, live, cux, cuy, &ux, &uy);
+#else
+    if (__any(!c.roles)) solve_newton<false>(pm, c, live, cux, cuy, &ux, &uy);
+    else solve_newton<true>(pm, c, live, cux, cuy, &ux, &uy);
+#endif
   }
   *wx = ux;
   *wy = uy;
