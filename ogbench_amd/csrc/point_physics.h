@@ -344,22 +344,19 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
   const bool vY = sy != 0 && ((m >> (4 + 3 * sy)) & 1u);
   const bool vD = sx != 0 && sy != 0 && ((m >> (4 + 3 * sy + sx)) & 1u);
   // x-side box: centre (cx + sx u, cy)
-  double dX, tXx, tXy;
+  // (its y offset is ly: the closest point's y is the centre's unless |ly| > hx,
+  // when tXy = clamp(ly) - ly != 0 and the face guard below routes to generic;
+  // otherwise tXy = ly - ly = +0 exactly, so it is not computed)
+  double dX, tXx;
   {
-    const double px = x - (cx + sx * u), py = y - cy;
-    const double clx = clamp_box(px, hx);
-    const double cly = clamp_box(py, hx);
-    tXx = clx - px;
-    tXy = cly - py;
+    const double px = x - (cx + sx * u);
+    tXx = clamp_box(px, hx) - px;
     dX = fabs(tXx);
   }
-  double dY, tYx, tYy;
+  double dY, tYy;
   {
-    const double px = x - cx, py = y - (cy + sy * u);
-    const double clx = clamp_box(px, hx);
-    const double cly = clamp_box(py, hx);
-    tYx = clx - px;
-    tYy = cly - py;
+    const double py = y - (cy + sy * u);
+    tYy = clamp_box(py, hx) - py;
     dY = fabs(tYy);
   }
   double tDx, tDy, d2D;
@@ -375,7 +372,7 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
   const bool cY = vY && dY - r <= 0.0;
   bool cD = vD && d2D <= pm.r2_hi;
   // exact-geometry guards: face roles must really be faces, d > mjMINVAL
-  slow = slow || (cX && (tXy != 0.0 || dX <= kMinVal)) || (cY && (tYx != 0.0 || dY <= kMinVal));
+  slow = slow || (cX && (fabs(ly) > hx || dX <= kMinVal)) || (cY && (fabs(lx) > hx || dY <= kMinVal));
   double dD = 0.0, nDx = 0.0, nDy = 0.0;
   OGBX_WSTAT(11, cD);
   OGBX_WSTAT(12, slow);
@@ -413,14 +410,14 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
   // s0: x face, n = (-sign(tx), -ty) with ty = +-0
   contact_gains(pm, dX - r, &D, &kp);
   c.s0.nx = cX ? (tXx > 0.0 ? -1.0 : 1.0) : 0.0;
-  c.s0.ny = cX ? -tXy : 0.0;
+  c.s0.ny = cX ? -0.0 : 0.0;  // -tXy, tXy = +0
   c.s0.tx = -c.s0.ny;
   c.s0.ty = c.s0.nx;
   c.s0.kp = cX ? kp : 0.0;
   c.s0.w = cX ? D : 0.0;
   // s1: y face
   contact_gains(pm, dY - r, &D, &kp);
-  c.s1.nx = cY ? -tYx : 0.0;
+  c.s1.nx = cY ? -0.0 : 0.0;  // -tYx, tYx = +0
   c.s1.ny = cY ? (tYy > 0.0 ? -1.0 : 1.0) : 0.0;
   c.s1.tx = -c.s1.ny;
   c.s1.ty = c.s1.nx;
