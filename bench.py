@@ -520,7 +520,8 @@ def cpu_baseline_gc(data, cfg, B, args):
 
 def bench_powder(args, world, rank, dev, level='easy'):
     """powderworld-{level}-v0, 64x64 worlds, N=4096 envs per GPU (SURVEY.md section 8 row b;
-    medium/hard: section 8f).  A step = one env.step of all envs (one step-kernel launch),
+    medium/hard: section 8f).  A step = one env.step of all envs (one step-kernel launch;
+    medium/hard: the render-only kernel then the full-rule kernel),
     uniformly random valid actions for the current stage, task i%5+1, same-step auto-reset
     (medium/hard: the auto-reset replays the task's goal in the same launch, as the
     reference's reset does)."""
@@ -530,7 +531,9 @@ def bench_powder(args, world, rank, dev, level='easy'):
     size = 64
     ne = {'easy': 2, 'medium': 5, 'hard': 8}[level]
     full = ne != 2
-    kern = 'pwf_step_kernel' if full else 'pw_step_kernel'
+    # medium/hard: a single step is two launches, the render-only kernel for envs
+    # whose step runs no forward and the full-rule kernel for the rest
+    kern = 'pwf_light_step_kernel+pwf_step_kernel' if full else 'pw_step_kernel'
     env = ogbench_amd.make(f'powderworld-{level}-v0', num_envs=n, device=dev, world_size=size, auto_reset=True)
     task = (torch.arange(n, dtype=torch.int32, device=dev) % 5) + 1
     env.reset(seed=rank, options=dict(task_id=task))

@@ -30,6 +30,7 @@
 // fully coalesced 16-byte stores (the obs write, 24 KB per 64x64 env-step, is
 // the HBM floor of the path).
 #include <array>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -633,11 +634,12 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     const int32_t* __restrict__ draws, const float* __restrict__ rand, int32_t k_steps, uint8_t* __restrict__ obs,
     float* __restrict__ reward, uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated,
     uint8_t* __restrict__ success, int32_t auto_reset, uint32_t k0, uint32_t k1, uint32_t a0, uint32_t a1,
-    uint32_t r0, uint32_t r1) {
+    uint32_t r0, uint32_t r1, const uint8_t* __restrict__ skip) {
   constexpr int C = WS * WS, CPT = FW<WS>::CPT;
   __shared__ PwFullShared<WS> sh;
   FW<WS> fw(sh);
   const int64_t e = blockIdx.x;
+  if (skip != nullptr && skip[e]) return;  // stepped by pwf_light_step_kernel
   pwf_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
   const int max_steps = Pp->max_steps;
@@ -728,6 +730,94 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     S.elapsed[e] = el;
     S.episode[e] = ep;
   }
+}
+
+// Render-only steps of medium/hard worlds (one step per launch).  An env at
+// stage 0 or 1 of the 3-step action machine that does not auto-reset this step
+// runs no forward: it draws its sub-action, advances the stage and renders its
+// unchanged world (powderworld_env.py:354-427, 462-476).  That needs 9 of the
+// 11 state bytes per cell and writes no state back, but inside
+// pwf_step_kernel it would hold the full rule set's 116 KB of LDS, i.e. one
+// env per CU with nothing to overlap its HBM round trips.  This kernel steps
+// those envs with a 24 KB staging buffer (6 envs per CU) and marks them in
+// `handled`; pwf_step_kernel, launched after it, skips the marked envs.  The
+// predicate is evaluated on the pre-step state by this kernel alone.
+template <int WS>
+__global__ void __launch_bounds__(256) pwf_light_step_kernel(
+    const PowderParams* __restrict__ Pp, PowderState S, const int32_t* __restrict__ action,
+    const int32_t* __restrict__ draws, uint8_t* __restrict__ obs, float* __restrict__ reward,
+    uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated, uint8_t* __restrict__ success,
+    int32_t auto_reset, uint32_t a0, uint32_t a1, uint8_t* __restrict__ handled) {
+  constexpr int C = WS * WS, CPT = C / 256;
+  __shared__ alignas(16) uint16_t st[C * 3];  // 6 observation bytes per cell
+  __shared__ uint32_t lut[32];
+  const int64_t e = blockIdx.x;
+  const int t = threadIdx.x;
+  if (t < 32) lut[t] = Pp->lut[t];
+  const int ctrl = S.ctrl[e];
+  int el = S.elapsed[e];
+  const uint32_t ep = S.episode[e];
+  int stage = ctrl & 3, elem = (ctrl >> 2) & 63, x = (ctrl >> 8) & 255;
+  const bool succ = (ctrl & kCtrlSuccess) != 0;
+  const bool full = stage == 2 || (auto_reset && (succ || el + 1 >= Pp->max_steps));
+  if (t == 0) handled[e] = full ? 0 : 1;
+  if (full) return;  // uniform over the workgroup
+  const int act = action[e];
+  if (stage == 0) {
+    const int ne = Pp->num_elems;
+    elem = act >= 0 && act < ne ? act : (draws ? draws[e] : (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)ne));
+  } else {
+    const int xy = Pp->xy_size;
+    x = act >= 0 && act < xy ? act : (draws ? draws[e] : (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)xy));
+  }
+  stage += 1;
+  el += 1;
+  const bool trunc = el >= Pp->max_steps;
+  if (t == 0) {
+    reward[e] = succ ? 1.0f : 0.0f;
+    terminated[e] = succ;
+    truncated[e] = trunc;
+    success[e] = succ;
+    S.ctrl[e] = stage | (elem << 2) | (x << 8) | (ctrl & (255 << 16)) | (succ ? kCtrlSuccess : 0);
+    S.elapsed[e] = el;
+  }
+  const uint32_t acol = Pp->lut[Pp->elem_ids[elem & 7] & 31];
+  const int rx = x * Pp->grid, brush = Pp->brush;
+  // thread t: cells [t*CPT, t*CPT + CPT) of one row
+  const int c0 = t * CPT;
+  const uint8_t* wa = S.world + (size_t)e * C + c0;
+  const float4* wv = reinterpret_cast<const float4*>(S.vel + (size_t)e * C + c0);
+  uint8_t ids[CPT];
+  if constexpr (CPT == 16) {
+    const uint4 q = *reinterpret_cast<const uint4*>(wa);
+    const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ids[k] = (uint8_t)(w4[k >> 2] >> (8 * (k & 3)));
+  } else {
+    const uint32_t q = *reinterpret_cast<const uint32_t*>(wa);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) ids[k] = (uint8_t)(q >> (8 * k));
+  }
+  float4 vv[CPT / 2];
+#pragma unroll
+  for (int k = 0; k < CPT / 2; ++k) vv[k] = wv[k];
+  __syncthreads();  // lut
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int i = c0 + k, col = i % WS;
+    const float2 v = (k & 1) ? make_float2(vv[k >> 1].z, vv[k >> 1].w) : make_float2(vv[k >> 1].x, vv[k >> 1].y);
+    const uint32_t c = pw_rgb(lut, fid(ids[k]), v);
+    const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
+    const uint32_t px = fr ? acol : 0u;
+    st[3 * i] = (uint16_t)(c & 0xffffu);
+    st[3 * i + 1] = (uint16_t)(((c >> 16) & 0xffu) | ((px & 0xffu) << 8));
+    st[3 * i + 2] = (uint16_t)((px >> 8) & 0xffffu);
+  }
+  __syncthreads();
+  const uint4* src = reinterpret_cast<const uint4*>(st);
+  uint4* d = reinterpret_cast<uint4*>(obs + (size_t)e * C * 6);
+#pragma unroll
+  for (int q = t; q < C * 6 / 16; q += 256) d[q] = src[q];
 }
 
 // Free-standing PWSim.forward on worlds in the reference's (n, 9, H, W)
@@ -947,6 +1037,8 @@ struct ogbx_powder_env {
   ogbx::PowderParams* Pd = nullptr;
   ogbx::PowderState S{};
   uint8_t* goals = nullptr;  // easy: [num_tasks, H*W] goal ids
+  uint8_t* handled = nullptr;  // medium/hard: [N] env stepped by pwf_light_step_kernel this launch
+  bool light = true;           // split render-only steps into pwf_light_step_kernel
   uint64_t seed = 0;
   bool was_reset = false;
 };
@@ -1060,6 +1152,8 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
     if (h == hipSuccess) h = hipMalloc(&e->S.mom, n * HW);
     if (h == hipSuccess) h = hipMalloc(&e->S.vel, n * HW * sizeof(float2));
     if (h == hipSuccess) h = hipMalloc(&e->S.goal_env, n * HW);
+    if (h == hipSuccess) h = hipMalloc(&e->handled, n);
+    if (const char* v = std::getenv("OGBX_PWF_LIGHT")) e->light = std::atoi(v) != 0;  // A/B knob
     if (h == hipSuccess) h = hipMemset(e->S.mom, 0, n * HW);
     if (h == hipSuccess) h = hipMemset(e->S.vel, 0, n * HW * sizeof(float2));
     if (h == hipSuccess) h = hipMemset(e->S.goal_env, 0, n * HW);
@@ -1091,6 +1185,7 @@ ogbx_status ogbx_powder_destroy(ogbx_powder_t e) {
   (void)hipFree(e->S.vel);
   (void)hipFree(e->S.goal_env);
   (void)hipFree(e->goals);
+  (void)hipFree(e->handled);
   delete e;
   return OGBX_OK;
 }
@@ -1156,8 +1251,15 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
   seed_key(e->seed, kTagPowderAction, &a0, &a1);
   seed_key(e->seed, kTagPowderRand, &r0, &r1);
   if (e->full) {
+    const bool light = e->light && k_steps == 1;
+    if (light) {
+      PW_LAUNCH(pwf_light_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, action, draws, obs, reward,
+                terminated, truncated, success, auto_reset, a0, a1, e->handled);
+      OGBX_LAUNCHED("pwf_light_step_kernel");
+    }
     PWF_LAUNCH(pwf_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps, obs,
-              reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1, r0, r1);
+              reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1, r0, r1,
+              light ? e->handled : (const uint8_t*)nullptr);
     OGBX_LAUNCHED("pwf_step_kernel");
   } else {
     PW_LAUNCH(pw_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs,

@@ -72,6 +72,24 @@ __constant__ float kPwColDev[21][3] = {
     {158 / 255.f, 157 / 255.f, 36 / 255.f},  {198 / 255.f, 40 / 255.f, 40 / 255.f},
     {224 / 255.f, 64 / 255.f, 251 / 255.f}};
 
+// Render colour of one cell (PWRenderer.render, sim.py:425-453): the exact
+// LUT colour at zero velocity, else the float32 blend toward the velocity
+// colour with d = clip(|v|/5, 0, 0.5), truncated to uint8.
+__device__ __forceinline__ uint32_t pw_rgb(const uint32_t* lut, uint32_t id, float2 v) {
+  if (v.x == 0.0f && v.y == 0.0f) return lut[id];
+  const float mag = sqrtf(v.x * v.x + v.y * v.y);
+  const float d = fminf(fmaxf(mag / 5.0f, 0.0f), 0.5f);
+  const float vc[3] = {200 / 255.f, 100 / 255.f, 100 / 255.f};
+  uint32_t out = 0;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    float x = (1.0f - d) * kPwColDev[id][ch] + d * vc[ch];
+    x = fminf(fmaxf(x, 0.0f), 1.0f);
+    out |= (uint32_t)(x * 255.0f) << (8 * ch);
+  }
+  return out;
+}
+
 // Rand-field purposes (Philox counter word w): goal replay forward s, the
 // reset's forward, the forward of elapsed step el.
 constexpr uint32_t kRandGoal = 1u << 24, kRandStart = 2u << 24, kRandStep = 3u << 24;
@@ -792,20 +810,7 @@ struct FullWorld {
 
   // PWRenderer colour of a cell, blended toward the velocity colour by
   // clip(|v| / 5, 0, 0.5) (sim.py:402-453), as R | G << 8 | B << 16.
-  __device__ __forceinline__ uint32_t rgb(uint32_t id, float2 v) const {
-    if (v.x == 0.0f && v.y == 0.0f) return s.lut[id];
-    const float mag = sqrtf(v.x * v.x + v.y * v.y);
-    const float d = fminf(fmaxf(mag / 5.0f, 0.0f), 0.5f);
-    const float vc[3] = {200 / 255.f, 100 / 255.f, 100 / 255.f};
-    uint32_t out = 0;
-#pragma unroll
-    for (int ch = 0; ch < 3; ++ch) {
-      float x = (1.0f - d) * kPwColDev[id][ch] + d * vc[ch];
-      x = fminf(fmaxf(x, 0.0f), 1.0f);
-      out |= (uint32_t)(x * 255.0f) << (8 * ch);
-    }
-    return out;
-  }
+  __device__ __forceinline__ uint32_t rgb(uint32_t id, float2 v) const { return pw_rgb(s.lut, id, v); }
 
   // Observation: RGB of the world + action frame (powderworld_env.py:462-476),
   // staged in LDS (6 bytes per cell as three 16-bit stores) and written as

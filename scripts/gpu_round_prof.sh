@@ -9,7 +9,7 @@ for wl in $WLS; do
   case $wl in
     pointmaze) K=maze_step_kernel; S=2000 ;;
     powder) K=pw_step_kernel; S=600 ;;
-    powder-medium|powder-hard) K=pwf_step_kernel; S=600 ;;
+    powder-medium|powder-hard) K=pwf_light_step_kernel+pwf_step_kernel; S=600 ;;
     gcsample) K=gc_sample_kernel; S=300 ;;
     hgcsample) K=hgc_sample_kernel; S=300 ;;
     *) echo "unknown workload $wl"; exit 2 ;;

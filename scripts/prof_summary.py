@@ -55,13 +55,22 @@ def main():
     stats = _one(os.path.join(a.out, f'prof_{a.workload}', '**', '*kernel_stats.csv'))
     dst = os.path.join(ROOT, 'profiles', f'{a.round}_{a.workload}_kernel_stats.csv')
     shutil.copyfile(stats, dst)
-    avg_ns = calls = None
     with open(stats) as f:
-        for row in csv.DictReader(f):
-            if a.kernel in row['Name']:
-                avg_ns, calls = float(row['AverageNs']), int(row['Calls'])
-    fetch, nf = counter_avg(os.path.join(a.out, f'pmc_fetch_{a.workload}'), 'FETCH_SIZE', a.kernel)
-    write, nw = counter_avg(os.path.join(a.out, f'pmc_write_{a.workload}'), 'WRITE_SIZE', a.kernel)
+        rows = list(csv.DictReader(f))
+    # '+'-joined kernels (a step made of several launches, one each per step):
+    # per-step duration and bytes are the sums over the parts
+    parts = a.kernel.split('+')
+    avg_ns, calls, fetch, write, nf, nw = 0.0, None, 0.0, 0.0, None, None
+    for k in parts:
+        for row in rows:
+            if k in row['Name']:
+                avg_ns += float(row['AverageNs'])
+                calls = int(row['Calls']) if calls is None else min(calls, int(row['Calls']))
+        fk, nfk = counter_avg(os.path.join(a.out, f'pmc_fetch_{a.workload}'), 'FETCH_SIZE', k)
+        wk, nwk = counter_avg(os.path.join(a.out, f'pmc_write_{a.workload}'), 'WRITE_SIZE', k)
+        fetch, write = fetch + fk, write + wk
+        nf = nfk if nf is None else min(nf, nfk)
+        nw = nwk if nw is None else min(nw, nwk)
     rec = dict(
         workload=a.workload,
         round=a.round,
