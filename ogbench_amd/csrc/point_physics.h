@@ -754,8 +754,16 @@ __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& 
 #endif
   }
   if (need_newton) {
+    // Every slot is evaluated: an empty slot is an all-zero row (r = 0, never
+    // active, no contribution).  Skipping slots no lane uses (three ballots and
+    // a uniform branch per slot and evaluation) measured 17 % slower: the
+    // branches break the straight-line schedule of the evaluations.
+#ifdef OGBX_LIVE_BALLOTS
     const uint32_t live = (__any(c.s0.w != 0.0) ? 1u : 0u) | (__any(c.s1.w != 0.0) ? 2u : 0u) |
                           (__any(c.s2.w != 0.0) ? 4u : 0u);
+#else
+    constexpr uint32_t live = 7u;
+#endif
 #ifdef OGBX_NO_ROLE_EVAL
     solve_newton<false>(pm, c, live, cux, cuy, &ux, &uy);
 #else

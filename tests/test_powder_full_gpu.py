@@ -256,3 +256,37 @@ def test_forward_rand_threshold_edges(gpu):
     for t in range(steps):
         ref = orc.forward(ref, [rand[t][:, k] for k in range(3)])
     assert np.array_equal(got, ref), _diff(got, ref)
+
+
+@pytest.mark.parametrize('ne,size', [(5, 64), (8, 32)])
+def test_mixed_stages_single_steps_match_fused(gpu, ne, size):
+    """Envs at different stages of the action machine in one launch: a single
+    step splits them between the render-only kernel (stage 0/1, no reset) and
+    the full-rule kernel; the fused rollout keeps all in one kernel.  Both from
+    the same state must agree bit for bit (outputs and final state)."""
+    n, K = 9, 15
+    a = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    a.reset(seed=21, options=dict(task_id=torch.arange(n, device=gpu) % 5 + 1))
+    rng = np.random.RandomState(9)
+    hi = max(ne, a._xy_action_size) + 1
+    for t in range(2):
+        a.step(rng.randint(0, hi, size=n))
+    # re-reset a third of the envs: stages 0 / 1 / 2 now coexist
+    a.reset(options=dict(task_id=3), mask=torch.tensor([i % 3 == 0 for i in range(n)], dtype=torch.uint8,
+                                                         device=gpu))
+    stages = (a.state_dict()['ctrl'] & 3).tolist()
+    assert len(set(stages)) >= 2, stages
+    b = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    b.reset(seed=21, options=dict(task_id=1))
+    b.load_state_dict(a.state_dict())
+    acts = rng.randint(0, hi, size=(K, n))
+    out = b.rollout(acts)
+    for t in range(K):
+        ob, rew, term, trunc, info = a.step(acts[t])
+        assert torch.equal(out['obs'][t], ob), t
+        assert torch.equal(out['reward'][t], rew), t
+        assert torch.equal(out['truncated'][t].bool(), trunc), t
+        assert torch.equal(out['success'][t].bool(), info['success']), t
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in ('world', 'ctrl', 'elapsed', 'episode', 'momentum', 'velocity', 'goal'):
+        assert torch.equal(sa[k], sb[k]), k
