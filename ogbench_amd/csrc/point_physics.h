@@ -149,6 +149,9 @@ __device__ __forceinline__ void contact_gains(const PointModel& pm, double dist,
   *D = pm.w_max;
   *kp = pm.kp_max * dist;
   const double x = fabs(dist) * pm.inv_width;
+#ifdef OGBX_ABL_NO_BAND
+  return;
+#endif
   if (x < 1.0) {
     double imp;
     if (x <= 0.0) {
@@ -401,9 +404,6 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
     }
   }
 #endif
-#ifndef OGBX_MICRO_NO_GENERIC
-  if (__builtin_expect(slow, 0)) return collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
-#endif
   OGBX_WSTAT(10, (cX && fabs(dX - r) * pm.inv_width < 1.0) || (cY && fabs(dY - r) * pm.inv_width < 1.0) ||
                      (cD && fabs(dD - r) * pm.inv_width < 1.0));
   double D, kp;
@@ -433,6 +433,11 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
   c.s2.w = cD ? D : 0.0;
   c.n = (int)cX + (int)cY + (int)cD;
   c.roles = true;
+#ifndef OGBX_MICRO_NO_GENERIC
+  // rare geometry: the generic collider replaces the role slots (placed after
+  // the straight-line role path rather than as an early exit: 7 % faster)
+  if (__builtin_expect(slow, 0)) collide_walls_generic(pm, nbmask, H, W, x, y, fi, fj, sx, sy, c);
+#endif
   return c.n;
 }
 
@@ -742,6 +747,16 @@ __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& 
   bool need_newton;
   OGBX_WSTAT(9, true);
   OGBX_WSTAT(8, c.n >= 2);
+#ifndef OGBX_CLOSED_FORM
+  // Every lane runs the (warm-started, straight-line) Newton solve, contact or
+  // not: the per-wave choice of the closed form for single-contact-only waves
+  // (25 % of wave-stages) cost more in branches than it saved (measured 4 %).
+  if (true) {
+    need_newton = true;
+    ux = c.n >= 1 ? *wx : cux;
+    uy = c.n >= 1 ? *wy : cuy;
+  } else
+#endif
   if (__any(c.n >= 2)) {
     need_newton = c.n >= 1;
     ux = c.n >= 1 ? *wx : cux;
@@ -767,8 +782,12 @@ __device__ __forceinline__ void solve_acc(const PointModel& pm, const Contacts& 
 #ifdef OGBX_NO_ROLE_EVAL
     solve_newton<false>(pm, c, live, cux, cuy, &ux, &uy);
 #else
+#ifdef OGBX_ABL_ROLES_ONLY
+    solve_newton<true>(pm, c, live, cux, cuy, &ux, &uy);
+#else
     if (__any(!c.roles)) solve_newton<false>(pm, c, live, cux, cuy, &ux, &uy);
     else solve_newton<true>(pm, c, live, cux, cuy, &ux, &uy);
+#endif
 #endif
   }
   *wx = ux;
