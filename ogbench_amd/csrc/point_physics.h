@@ -825,7 +825,12 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
   const int nstage = 4 * pm.nsub;
 #endif
   OGBX_STAT(6);
-#pragma unroll 1
+#ifndef OGBX_STAGE_UNROLL
+// Unrolled by the RK stage count: the stage index (and its A/B coefficients,
+// the e != 0 collide test) become constants (1.71 -> 1.77 G env-steps/s).
+#define OGBX_STAGE_UNROLL 4
+#endif
+#pragma unroll OGBX_STAGE_UNROLL
   for (int e = 0; e < nstage; ++e) {
     const int st = e & 3;
     double fx, fy;
