@@ -185,8 +185,20 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+_dev_index = {}
+
+
 def stream_of(device):
-    """hipStream_t of torch's current stream on `device`, as a void*."""
+    """hipStream_t of torch's current stream on `device`, as a void*.
+
+    Reads the raw stream handle (no torch.cuda.Stream object per call: that
+    costs microseconds, the same order as a latency-bound sampler launch)."""
     import torch
 
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    idx = _dev_index.get(device)
+    if idx is None:
+        d = torch.device('cuda', device) if isinstance(device, int) else torch.device(device)
+        if d.index is None:  # 'cuda': the current device, which may change
+            return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(torch.cuda.current_device()))
+        idx = _dev_index[device] = d.index
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(idx))

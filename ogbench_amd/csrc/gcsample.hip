@@ -41,11 +41,12 @@ struct GoalDraws {
 };
 
 // GCDataset.sample_goals for one sample (datasets.py:296-327).
+// rand_goal = valid_idxs[d.pick] (or d.pick), loaded by the caller together
+// with the sample's other index loads.
 __device__ inline int64_t sample_goal(int64_t idx, int64_t final_idx, const GoalDraws& d,
-                                      const int64_t* valid_idxs, int64_t num_valid,
-                                      double p_cur, double thresh, int geom, int cur_is_one) {
+                                      int64_t rand_goal, double p_cur, double thresh, int geom,
+                                      int cur_is_one) {
   if (cur_is_one) return idx;
-  const int64_t rand_goal = valid_idxs ? valid_idxs[d.pick] : d.pick;
   int64_t traj;
   if (geom) {
     const int64_t s = idx + d.geom;
@@ -57,6 +58,32 @@ __device__ inline int64_t sample_goal(int64_t idx, int64_t final_idx, const Goal
   int64_t goal = d.u_traj < thresh ? traj : rand_goal;
   goal = d.u_cur < p_cur ? idx : goal;
   return goal;
+}
+
+// The sample's dependent index loads, issued back to back so that they share
+// one HBM round trip: idx = valid_idxs[pick], its trajectory end, and the
+// random goals valid_idxs[goal pick] (datasets.py:65-70, 307-309).  Every
+// condition is wave-uniform (pointer presence), so no load address waits on
+// another load; for explicit idxs (pick < 0) the end needs idx first.
+__device__ inline void index_loads(const ogbx_gc_buffer& buf, bool explicit_idxs, int64_t pick,
+                                   int64_t* idx, int64_t* fin) {
+  const int64_t* __restrict__ vi = buf.valid_idxs;
+  if (explicit_idxs) {
+    *fin = buf.traj_end[*idx];
+  } else if (vi && buf.valid_traj_end) {
+    *idx = vi[pick];
+    *fin = buf.valid_traj_end[pick];
+  } else if (vi) {
+    *idx = vi[pick];
+    *fin = buf.traj_end[*idx];
+  } else {
+    *idx = pick;
+    *fin = buf.traj_end[pick];
+  }
+}
+
+__device__ inline int64_t rand_goal_of(const ogbx_gc_buffer& buf, int64_t pick) {
+  return buf.valid_idxs ? buf.valid_idxs[pick] : pick;
 }
 
 __device__ inline int64_t geometric_from(double u, double log_q) {
@@ -87,48 +114,50 @@ __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, 
 }
 
 // Copy every column row of a tile.  For small tiles (latency-bound launches)
-// whose columns are all 4-byte granular (float32 data), the (column, sample,
-// word) items of the whole tile form one
-// flat index space and each thread issues kUnroll loads before its stores, so
-// the columns' HBM round trips overlap instead of running one after another.
+// whose columns are all 4-byte granular with rows of <= 128 words, each
+// (column, sample) row is one job for one wave: the job's column descriptor
+// and row index are wave-uniform (scalar loads, one LDS broadcast), lanes
+// cover the row's words, and each wave issues the loads of up to kJ jobs
+// before any store, so all column rows of the tile share one HBM round trip.
 // Otherwise each column is copied with its widest aligned unit.
 template <int kSel>
 __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int64_t (*sel)[kGcMaxTile], int64_t base,
                                  int n_here, bool flat4) {
   if (flat4) {
-    constexpr int kUnroll = 4;
-    __shared__ int s_pre[kGcMaxCols + 1];
-    if (threadIdx.x == 0) {
-      int acc = 0;
-      for (int c = 0; c < num_cols; ++c) {
-        s_pre[c] = acc;
-        acc += (int)(cols.c[c].row_bytes >> 2) * n_here;
-      }
-      s_pre[num_cols] = acc;
-    }
-    __syncthreads();
-    const int total = s_pre[num_cols];
-    for (int f0 = threadIdx.x; f0 < total; f0 += blockDim.x * kUnroll) {
-      uint32_t v[kUnroll];
-      uint32_t* d[kUnroll];
+    constexpr int kJ = 8, kSlots = 2;
+    const int nw = (int)(blockDim.x >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = (int)(threadIdx.x & 63);
+    const int jobs = num_cols * n_here;
+    for (int j0 = wave; j0 < jobs; j0 += nw * kJ) {
+      uint32_t v[kJ][kSlots];
+      uint32_t* d[kJ][kSlots];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
-        const int f = f0 + u * (int)blockDim.x;
-        d[u] = nullptr;
-        if (f < total) {
-          int c = 0;
-          while (s_pre[c + 1] <= f) ++c;
+      for (int u = 0; u < kJ; ++u) {
+        const int j = j0 + u * nw;
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q) d[u][q] = nullptr;
+        if (j < jobs) {
+          const int c = j / n_here, b = j - c * n_here;
           const ogbx_gc_column& col = cols.c[c];
           const int units = (int)(col.row_bytes >> 2);
-          const int rel = f - s_pre[c];
-          const int b = rel / units, k = rel - b * units;
-          v[u] = ((const uint32_t*)col.src)[sel[col.select][b] * units + k];
-          d[u] = (uint32_t*)col.dst + (base + b) * units + k;
+          const uint32_t* src = (const uint32_t*)col.src + sel[col.select][b] * units;
+          uint32_t* dst = (uint32_t*)col.dst + (base + b) * units;
+#pragma unroll
+          for (int q = 0; q < kSlots; ++q) {
+            const int k = lane + 64 * q;
+            if (k < units) {
+              v[u][q] = src[k];
+              d[u][q] = dst + k;
+            }
+          }
         }
       }
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u)
-        if (d[u]) *d[u] = v[u];
+      for (int u = 0; u < kJ; ++u)
+#pragma unroll
+        for (int q = 0; q < kSlots; ++q)
+          if (d[u][q]) *d[u][q] = v[u][q];
     }
     return;
   }
@@ -147,6 +176,7 @@ __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int6
   }
 }
 
+template <bool kInj>
 __global__ void __launch_bounds__(256) gc_sample_kernel(
     ogbx_gc_buffer buf, ogbx_gc_config cfg, GcColumns cols, int32_t num_cols, int64_t total,
     int tile, ogbx_gc_draws dr, uint32_t k0, uint32_t k1, uint32_t call_lo, uint32_t call_hi,
@@ -166,33 +196,29 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
     const u32x4 w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
     const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
     // sample index (datasets.py:65-70)
-    int64_t idx, pick = -1;
-    if (dr.idxs) {
-      idx = dr.idxs[s];
-    } else {
-      pick = dr.pick ? dr.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
-      idx = buf.valid_idxs ? buf.valid_idxs[pick] : pick;
-    }
-    const int64_t final_idx = (pick >= 0 && buf.valid_traj_end) ? buf.valid_traj_end[pick] : buf.traj_end[idx];
-    const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
+    int64_t idx = 0, pick = -1, final_idx;
+    if (kInj && dr.idxs) idx = dr.idxs[s];
+    else pick = (kInj && dr.pick) ? dr.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
     GoalDraws v, a;
-    v.pick = dr.v_pick ? dr.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
-    a.pick = dr.a_pick ? dr.a_pick[s] : (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+    v.pick = (kInj && dr.v_pick) ? dr.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
+    a.pick = (kInj && dr.a_pick) ? dr.a_pick[s] : (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+    index_loads(buf, kInj && dr.idxs != nullptr, pick, &idx, &final_idx);
+    const int64_t v_rand = cfg.value_cur_is_one ? 0 : rand_goal_of(buf, v.pick);
+    const int64_t a_rand = cfg.actor_cur_is_one ? 0 : rand_goal_of(buf, a.pick);
+    const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
     const double uvg = u01_from(w1.z, w1.w), uag = u01_from(w2.x, w2.y);
-    v.geom = dr.v_geom ? dr.v_geom[s] : (cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0);
-    a.geom = dr.a_geom ? dr.a_geom[s] : (cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0);
-    v.dist = dr.v_dist ? dr.v_dist[s] : uvg;
-    a.dist = dr.a_dist ? dr.a_dist[s] : uag;
-    v.u_traj = dr.v_u_traj ? dr.v_u_traj[s] : u01_from(w2.z, w2.w);
-    v.u_cur = dr.v_u_cur ? dr.v_u_cur[s] : u01_from(w3.x, w3.y);
-    a.u_traj = dr.a_u_traj ? dr.a_u_traj[s] : u01_from(w3.z, w3.w);
-    a.u_cur = dr.a_u_cur ? dr.a_u_cur[s] : u01_from(w4.x, w4.y);
-    const int64_t vg = sample_goal(idx, final_idx, v, buf.valid_idxs, buf.num_valid,
-                                   cfg.value_p_curgoal, cfg.value_traj_thresh,
-                                   cfg.value_geom_sample, cfg.value_cur_is_one);
-    const int64_t ag = sample_goal(idx, final_idx, a, buf.valid_idxs, buf.num_valid,
-                                   cfg.actor_p_curgoal, cfg.actor_traj_thresh,
-                                   cfg.actor_geom_sample, cfg.actor_cur_is_one);
+    v.geom = (kInj && dr.v_geom) ? dr.v_geom[s] : (cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0);
+    a.geom = (kInj && dr.a_geom) ? dr.a_geom[s] : (cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0);
+    v.dist = (kInj && dr.v_dist) ? dr.v_dist[s] : uvg;
+    a.dist = (kInj && dr.a_dist) ? dr.a_dist[s] : uag;
+    v.u_traj = (kInj && dr.v_u_traj) ? dr.v_u_traj[s] : u01_from(w2.z, w2.w);
+    v.u_cur = (kInj && dr.v_u_cur) ? dr.v_u_cur[s] : u01_from(w3.x, w3.y);
+    a.u_traj = (kInj && dr.a_u_traj) ? dr.a_u_traj[s] : u01_from(w3.z, w3.w);
+    a.u_cur = (kInj && dr.a_u_cur) ? dr.a_u_cur[s] : u01_from(w4.x, w4.y);
+    const int64_t vg = sample_goal(idx, final_idx, v, v_rand, cfg.value_p_curgoal,
+                                   cfg.value_traj_thresh, cfg.value_geom_sample, cfg.value_cur_is_one);
+    const int64_t ag = sample_goal(idx, final_idx, a, a_rand, cfg.actor_p_curgoal,
+                                   cfg.actor_traj_thresh, cfg.actor_geom_sample, cfg.actor_cur_is_one);
     sel[0][threadIdx.x] = idx;
     sel[1][threadIdx.x] = next;
     sel[2][threadIdx.x] = vg;
@@ -235,6 +261,7 @@ constexpr int kHgcSel = 10;
 
 // HGCDataset.sample (datasets.py:496-643): same tile structure as
 // gc_sample_kernel with ten row selectors and the hierarchical scalars.
+template <bool kInj>
 __global__ void __launch_bounds__(256) hgc_sample_kernel(
     ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, GcColumns cols, int32_t num_cols,
     int64_t total, int tile, ogbx_hgc_draws dr, uint32_t k0, uint32_t k1, uint32_t call_lo,
@@ -254,42 +281,45 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     const u32x4 w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
     const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
     const ogbx_gc_draws& g = dr.gc;
-    int64_t idx, pick = -1;
-    if (g.idxs) {
-      idx = g.idxs[s];
-    } else {
-      pick = g.pick ? g.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
-      idx = buf.valid_idxs ? buf.valid_idxs[pick] : pick;
-    }
-    const int64_t fin = (pick >= 0 && buf.valid_traj_end) ? buf.valid_traj_end[pick] : buf.traj_end[idx];
-    const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
+    int64_t idx = 0, pick = -1, fin;
+    if (kInj && g.idxs) idx = g.idxs[s];
+    else pick = (kInj && g.pick) ? g.pick[s] : (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
     GoalDraws v, a, l;
-    v.pick = g.v_pick ? g.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
-    a.pick = g.a_pick ? g.a_pick[s] : (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+    v.pick = (kInj && g.v_pick) ? g.v_pick[s] : (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
+    a.pick = (kInj && g.a_pick) ? g.a_pick[s] : (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+    u32x4 w5{}, w6{};
+    int64_t l_rand = 0;
+    if (hc.has_low_value_goals) {
+      w5 = philox4x32_10({c0, call_lo, 5u, c3}, k0, k1);
+      w6 = philox4x32_10({c0, call_lo, 6u, c3}, k0, k1);
+      l.pick = (kInj && dr.l_pick) ? dr.l_pick[s] : (int64_t)bounded64(w5.x, w5.y, (uint64_t)npick);
+    }
+    index_loads(buf, kInj && g.idxs != nullptr, pick, &idx, &fin);
+    const int64_t v_rand = cfg.value_cur_is_one ? 0 : rand_goal_of(buf, v.pick);
+    const int64_t a_rand = cfg.actor_cur_is_one ? 0 : rand_goal_of(buf, a.pick);
+    if (hc.has_low_value_goals && !cfg.value_cur_is_one) l_rand = rand_goal_of(buf, l.pick);
+    const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
     const double uvg = u01_from(w1.z, w1.w), uag = u01_from(w2.x, w2.y);
-    v.geom = g.v_geom ? g.v_geom[s] : (cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0);
-    a.geom = g.a_geom ? g.a_geom[s] : (cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0);
-    v.dist = g.v_dist ? g.v_dist[s] : uvg;
-    a.dist = g.a_dist ? g.a_dist[s] : uag;
-    v.u_traj = g.v_u_traj ? g.v_u_traj[s] : u01_from(w2.z, w2.w);
-    v.u_cur = g.v_u_cur ? g.v_u_cur[s] : u01_from(w3.x, w3.y);
-    a.u_traj = g.a_u_traj ? g.a_u_traj[s] : u01_from(w3.z, w3.w);
-    a.u_cur = g.a_u_cur ? g.a_u_cur[s] : u01_from(w4.x, w4.y);
-    const int64_t hvg = sample_goal(idx, fin, v, buf.valid_idxs, buf.num_valid, cfg.value_p_curgoal,
-                                    cfg.value_traj_thresh, cfg.value_geom_sample, cfg.value_cur_is_one);
-    const int64_t hag = sample_goal(idx, fin, a, buf.valid_idxs, buf.num_valid, cfg.actor_p_curgoal,
-                                    cfg.actor_traj_thresh, cfg.actor_geom_sample, cfg.actor_cur_is_one);
+    v.geom = (kInj && g.v_geom) ? g.v_geom[s] : (cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0);
+    a.geom = (kInj && g.a_geom) ? g.a_geom[s] : (cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0);
+    v.dist = (kInj && g.v_dist) ? g.v_dist[s] : uvg;
+    a.dist = (kInj && g.a_dist) ? g.a_dist[s] : uag;
+    v.u_traj = (kInj && g.v_u_traj) ? g.v_u_traj[s] : u01_from(w2.z, w2.w);
+    v.u_cur = (kInj && g.v_u_cur) ? g.v_u_cur[s] : u01_from(w3.x, w3.y);
+    a.u_traj = (kInj && g.a_u_traj) ? g.a_u_traj[s] : u01_from(w3.z, w3.w);
+    a.u_cur = (kInj && g.a_u_cur) ? g.a_u_cur[s] : u01_from(w4.x, w4.y);
+    const int64_t hvg = sample_goal(idx, fin, v, v_rand, cfg.value_p_curgoal, cfg.value_traj_thresh,
+                                    cfg.value_geom_sample, cfg.value_cur_is_one);
+    const int64_t hag = sample_goal(idx, fin, a, a_rand, cfg.actor_p_curgoal, cfg.actor_traj_thresh,
+                                    cfg.actor_geom_sample, cfg.actor_cur_is_one);
     int64_t lvg = idx;
     if (hc.has_low_value_goals) {
-      const u32x4 w5 = philox4x32_10({c0, call_lo, 5u, c3}, k0, k1);
-      const u32x4 w6 = philox4x32_10({c0, call_lo, 6u, c3}, k0, k1);
-      l.pick = dr.l_pick ? dr.l_pick[s] : (int64_t)bounded64(w5.x, w5.y, (uint64_t)npick);
-      l.geom = dr.l_geom ? dr.l_geom[s] : geometric_from(u01_from(w5.z, w5.w), l_log_q);
+      l.geom = (kInj && dr.l_geom) ? dr.l_geom[s] : geometric_from(u01_from(w5.z, w5.w), l_log_q);
       l.dist = 0.0;
-      l.u_traj = dr.l_u_traj ? dr.l_u_traj[s] : u01_from(w6.x, w6.y);
-      l.u_cur = dr.l_u_cur ? dr.l_u_cur[s] : u01_from(w6.z, w6.w);
-      lvg = sample_goal(idx, fin, l, buf.valid_idxs, buf.num_valid, cfg.value_p_curgoal,
-                        cfg.value_traj_thresh, 1, cfg.value_cur_is_one);
+      l.u_traj = (kInj && dr.l_u_traj) ? dr.l_u_traj[s] : u01_from(w6.x, w6.y);
+      l.u_cur = (kInj && dr.l_u_cur) ? dr.l_u_cur[s] : u01_from(w6.z, w6.w);
+      lvg = sample_goal(idx, fin, l, l_rand, cfg.value_p_curgoal, cfg.value_traj_thresh, 1,
+                        cfg.value_cur_is_one);
       if (rec.l_pick) {
         rec.l_pick[s] = l.pick;
         rec.l_geom[s] = l.geom;
@@ -376,16 +406,21 @@ struct PositiveF32 {
 
 using namespace ogbx;
 
-// Every column 4-byte granular and aligned, and the tile's word count small
-// enough for the flat int indexing of copy_tile.
+// Every column 4-byte granular and aligned with rows of <= 128 words (the
+// per-wave job copy of copy_tile).
 static bool flat4_columns(const GcColumns& cc, int num_cols) {
-  int64_t words = 0;
   for (int i = 0; i < num_cols; ++i) {
     const ogbx_gc_column& c = cc.c[i];
-    if (c.row_bytes % 4 != 0 || ((uintptr_t)c.src | (uintptr_t)c.dst) % 4 != 0) return false;
-    words += (c.row_bytes >> 2) * kGcMaxTile;
+    if (c.row_bytes % 4 != 0 || c.row_bytes > 512 || ((uintptr_t)c.src | (uintptr_t)c.dst) % 4 != 0) return false;
   }
-  return words < (1ll << 30);
+  return true;
+}
+
+// True when any draw is injected (parity replays); the Philox-only kernels
+// carry no per-draw pointer tests, so their index loads issue back to back.
+static bool any_draw(const ogbx_gc_draws& d) {
+  return d.idxs || d.pick || d.v_pick || d.v_geom || d.v_dist || d.v_u_traj || d.v_u_cur ||
+         d.a_pick || d.a_geom || d.a_dist || d.a_u_traj || d.a_u_cur;
 }
 
 extern "C" {
@@ -424,7 +459,8 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
   seed_key(seed, kTagGcSample, &k0, &k1);
   const double v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
   const double a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
-  hipLaunchKernelGGL(gc_sample_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
+  auto kern = any_draw(dr) ? gc_sample_kernel<true> : gc_sample_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream,
                      *buf, *cfg, cc, num_cols, total, (int)tile, dr, k0, k1,
                      (uint32_t)call_index, (uint32_t)(call_index >> 32), v_log_q, a_log_q,
                      idxs_out, value_goal_out, actor_goal_out, masks, rewards, rec,
@@ -476,7 +512,9 @@ ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg
   const double v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
   const double a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
   const double l_log_q = hcfg->has_low_value_goals ? std::log(1.0 - (1.0 - hcfg->low_discount)) : 0.0;
-  hipLaunchKernelGGL(hgc_sample_kernel, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, *buf,
+  const bool inj = any_draw(dr.gc) || dr.l_pick || dr.l_geom || dr.l_u_traj || dr.l_u_cur;
+  auto kern = inj ? hgc_sample_kernel<true> : hgc_sample_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, *buf,
                      *cfg, *hcfg, cc, num_cols, total, (int)tile, dr, k0, k1, (uint32_t)call_index,
                      (uint32_t)(call_index >> 32), v_log_q, a_log_q, l_log_q, *out, rec,
                      tile <= 4 && flat4_columns(cc, num_cols));

@@ -253,7 +253,6 @@ class GCDataset:
         self._calls = 0
         self._plain = _plain
         self._out_cache = {}
-        self._no_draws = GcDraws()
 
     # ---------------------------------------------------------------- helpers
     def _p_aug_draw(self, out, evaluation):
@@ -313,12 +312,11 @@ class GCDataset:
         if out is not None and plain_call:
             hit = self._out_cache.get(id(out))
             if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
-                _, _, col_arr, ncols, masks, rewards, idx_out = hit
+                col_p, ncols, idx_p, masks_p, rewards_p = hit[2]
                 seed, call = self._next_seed()
                 _lib.check(self._L.ogbx_gc_sample(
-                    self._buf, self._cfg, ctypes.cast(col_arr, ctypes.c_void_p), ncols, int(batch_size),
-                    int(num_batches), self._no_draws, seed, call, _lib.ptr(idx_out), None, None,
-                    _lib.ptr(masks), _lib.ptr(rewards), None, _lib.stream_of(self.device)), 'gc_sample')
+                    self._buf, self._cfg, col_p, ncols, int(batch_size), int(num_batches), None, seed, call,
+                    idx_p, None, None, masks_p, rewards_p, None, _lib.stream_of(self.device)), 'gc_sample')
                 self._p_aug_draw(out, evaluation)
                 return out
         out, cols = self._columns(total, _keys)
@@ -365,7 +363,10 @@ class GCDataset:
             # remember the descriptors so that sample(..., out=this) skips setup
             if len(self._out_cache) >= 2:
                 self._out_cache.clear()
-            self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), col_arr, len(cols), masks, rewards,
+            # (the output tensors stay alive in `out`; col_arr is kept for its pointer)
+            fast = (ctypes.cast(col_arr, ctypes.c_void_p), len(cols), _lib.ptr(idx_out), _lib.ptr(masks),
+                    _lib.ptr(rewards))
+            self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), fast, col_arr, masks, rewards,
                                         idx_out)
         if self._plain:
             return out
@@ -526,11 +527,12 @@ class HGCDataset(GCDataset):
         plain_call = idxs is None and not draws and not record_draws
         hit = self._out_cache.get(id(out)) if (out is not None and plain_call) else None
         if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
-            _, _, col_arr, ncols, outs = hit
-            dr, rec, keep = HgcDraws(), None, []
+            _, _, col_arr, ncols, outs, _ = hit
+            dr, rec, keep = None, None, []
         else:
             out, cols = self._hcolumns(total)
-            col_arr = (GcColumn * max(1, len(cols)))(*cols)
+            col_keep = (GcColumn * max(1, len(cols)))(*cols)
+            col_arr = ctypes.cast(col_keep, ctypes.c_void_p)
             ncols = len(cols)
             ptr = lambda k: out[k].data_ptr() if k in out else None  # noqa: E731
             outs = HgcOutputs(None, None, None, None, *[ptr(k) for k in _HGC_SCALARS[4:]])
@@ -560,10 +562,10 @@ class HGCDataset(GCDataset):
             if plain_call:
                 if len(self._out_cache) >= 2:
                     self._out_cache.clear()
-                self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), col_arr, ncols, outs)
+                self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), col_arr, ncols, outs, col_keep)
         seed, call = self._next_seed()
         _lib.check(self._Lh.ogbx_hgc_sample(
-            self._buf, self._cfg, self._hcfg, ctypes.cast(col_arr, ctypes.c_void_p), ncols, int(batch_size),
+            self._buf, self._cfg, self._hcfg, col_arr, ncols, int(batch_size),
             int(num_batches), dr, seed, call, outs, rec, _lib.stream_of(self.device)), 'hgc_sample')
         self._p_aug_draw(out, evaluation)
         if record_draws:
