@@ -164,6 +164,13 @@ class MazeEnv:
         self._term = torch.zeros(n, dtype=torch.uint8, **kw)
         self._trunc = torch.zeros(n, dtype=torch.uint8, **kw)
         self._succ = torch.zeros(n, dtype=torch.uint8, **kw)
+        # step() outputs are fixed buffers: their pointers and bool views once
+        self._step_out = (_lib.ptr(self._obs), _lib.ptr(self._reward), _lib.ptr(self._term),
+                          _lib.ptr(self._trunc), _lib.ptr(self._succ),
+                          _lib.ptr(self._final_obs))  # written only by an auto-reset
+        self._term_b = self._term.view(torch.bool)
+        self._trunc_b = self._trunc.view(torch.bool)
+        self._succ_b = self._succ.view(torch.bool)
         self._seed = None
         self._init_seed = seed
         self._has_reset = False
@@ -410,25 +417,14 @@ class MazeEnv:
             raise ValueError(f'action must have shape ({self.num_envs}, 2), got {tuple(a.shape)}')
         _lib.check(
             self._L.ogbx_maze_step(
-                self._h,
-                _lib.ptr(a),
-                int(a.dtype == _torch().float64),
-                1,
-                _lib.ptr(self._obs),
-                _lib.ptr(self._reward),
-                _lib.ptr(self._term),
-                _lib.ptr(self._trunc),
-                _lib.ptr(self._succ),
-                _lib.ptr(self._final_obs) if self.auto_reset else None,
-                int(self.auto_reset),
-                self._stream(),
-            ),
+                self._h, a.data_ptr(), int(a.dtype == _torch().float64), 1, *self._step_out,
+                int(self.auto_reset), self._stream()),
             'step',
         )
-        info = {'success': self._succ.view(_torch().bool)}
+        info = {'success': self._succ_b}
         if self.auto_reset:
             info['final_observation'] = self._final_obs
-        return self._obs, self._reward, self._term.view(_torch().bool), self._trunc.view(_torch().bool), info
+        return self._obs, self._reward, self._term_b, self._trunc_b, info
 
     def rollout(self, actions, out=None):
         """K fused steps in ONE launch: actions [K,N,2] -> per-step outputs [K,N,...].
