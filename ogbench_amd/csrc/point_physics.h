@@ -808,12 +808,24 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
   CellFrame fr;
   OGBX_STAMP_DECL
   cell_frame(pm, wall, H, W, x, y, fr);
-  if (collide_in_frame(pm, wall, H, W, x, y, fr, c) == 0) {
+  const bool in_contact = collide_in_frame(pm, wall, H, W, x, y, fr, c) != 0;
+#ifdef OGBX_MASKED_FREE
+  if (!in_contact) {
+#else
+  // Free lanes of a wave with a contact lane run the contact loop too (their
+  // result is discarded below): gfx950 issues a dependent VALU chain about 2x
+  // slower when only a few lanes of the wave are active (<= 8 for fp64 ops,
+  // <= 16 for 32-bit ops; scripts/micro/lane_count.hip), and the contact loop
+  // is exactly such a chain.  The chain length, not the lane count, sets the
+  // wave's time, so the extra lanes cost nothing.
+  if (!__any(in_contact)) {
+#endif
     *px = x + 0.0;
     *py = y + 0.0;
     OGBX_STAMP_END;
     return 0;
   }
+  const double x0 = x, y0 = y;
   const double h = pm.h;
   double vx = 0.0, vy = 0.0;                          // X[0] velocity of the substep
   double qsx = x, qsy = y, vsx = 0.0, vsy = 0.0;      // state of the current RK stage
@@ -872,9 +884,10 @@ __device__ __forceinline__ int point_step(const PointModel& pm, const uint16_t* 
     OGBX_STAMP_SEG(_tc);
   }
   OGBX_STAMP_END;
-  *px = x;
-  *py = y;
-  return 1;
+  // lanes that started free keep the exact free step (qpos + 0.0)
+  *px = in_contact ? x : x0 + 0.0;
+  *py = in_contact ? y : y0 + 0.0;
+  return in_contact ? 1 : 0;
 }
 
 // MuJoCo-derived constants of the point model (DESIGN.md lists each source).
