@@ -52,6 +52,34 @@ def test_physics_matches_oracle_with_contacts(gpu, maze, f64):
     assert np.array_equal(got[rc == 0], ref[rc == 0])
 
 
+@pytest.mark.parametrize('k', [1, 8, 63])
+def test_physics_waves_mixing_contact_and_free_lanes(gpu, k):
+    """Waves of 64 envs with exactly k contact lanes: the free lanes run the
+    contact loop alongside (point_step) and must still return the exact free
+    step and contact flag 0; the contact lanes match the oracle."""
+    rng = np.random.RandomState(100 + k)
+    mp, _ = orc.tables('large')
+    cells = np.argwhere(mp == 0)
+    n = 40000
+    c = cells[rng.randint(len(cells), size=n)]
+    q = np.stack([c[:, 1] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n), c[:, 0] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n)], 1)
+    a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+    _, rc = orc.physics('large', q, a, nthreads=8)
+    ci, fi = np.flatnonzero(rc == 1), np.flatnonzero(rc == 0)
+    waves = min(len(ci) // k, len(fi) // (64 - k), 128)
+    order = np.concatenate([np.concatenate([ci[w * k:(w + 1) * k], fi[w * (64 - k):(w + 1) * (64 - k)]])
+                            for w in range(waves)])
+    qm, am = q[order], a[order]
+    env = _env(gpu, 1)
+    out, contact = env.physics(torch.tensor(qm), torch.tensor(am))
+    ref, rcm = orc.physics('large', qm, am, nthreads=8)
+    got = out.cpu().numpy()
+    assert np.array_equal(contact.cpu().numpy(), rcm)
+    assert rcm.reshape(waves, 64).sum(1).tolist() == [k] * waves
+    assert np.array_equal(got[rcm == 0], ref[rcm == 0])
+    assert np.abs(got - ref).max() <= TOL
+
+
 def test_xy_to_ij_bit_exact(gpu, golden_locomaze):
     env = _env(gpu, 1)
     ij = env.xy_to_ij(torch.tensor(golden_locomaze['xy2ij_in']))
