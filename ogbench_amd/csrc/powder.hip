@@ -448,6 +448,7 @@ __global__ void __launch_bounds__(256) pw_step_kernel(
   __shared__ PwShared<WS> sh;
   Blk<WS> b(sh);
   const int64_t e = blockIdx.x;
+  const int act0 = action[e];  // first step's action, loaded with the world (not after the barrier)
   load_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
   const int max_steps = Pp->max_steps, tol = Pp->tol;
@@ -462,7 +463,7 @@ __global__ void __launch_bounds__(256) pw_step_kernel(
   __syncthreads();
   for (int k = 0; k < k_steps; ++k) {
     const int64_t o = (int64_t)k * n + e;
-    const int act = action[o];
+    const int act = k == 0 ? act0 : action[o];
     int stage = ctrl & 3, elem = (ctrl >> 2) & 63, x = (ctrl >> 8) & 255;
     bool succ = (ctrl & kCtrlSuccess) != 0;
     auto rnd = [&](int bound) -> int {
