@@ -63,13 +63,19 @@ struct PointModel {
 
 constexpr double kMinVal = 1e-15;  // mjMINVAL
 
-// 1/d for d > 0 in the normal range: v_rcp_f64 + two Newton-Raphson
-// refinements (5 dependent instructions instead of the 10 of the IEEE
-// division sequence; within an ulp of the quotient).
+// 1/d for d > 0 in the normal range: v_rcp_f64 + one Newton-Raphson
+// refinement (3 dependent instructions instead of the 10 of the IEEE division
+// sequence).  Measured on gfx950 (scripts/micro/rcp_err.hip, 4M values over
+// [2^-20, 2^20)): v_rcp_f64 alone 4.6e-8 relative error, +1 refinement
+// 2.2e-15 (10 ulp), +2 refinements equal to 1.0/d.  The second refinement
+// cost 0.8 % of the step and changes no parity result at the 1e-9 contact
+// tolerance (-DOGBX_RCP_NR2 restores it).
 __device__ __forceinline__ double fast_recip(double d) {
   double r = __builtin_amdgcn_rcp(d);
   r = fma(r, fma(-d, r, 1.0), r);
+#ifdef OGBX_RCP_NR2
   r = fma(r, fma(-d, r, 1.0), r);
+#endif
   return r;
 }
 
