@@ -62,6 +62,9 @@ struct PointModel {
 };
 
 constexpr double kMinVal = 1e-15;  // mjMINVAL
+// Largest double x with fl(sqrt(x)) <= 0.7 (the point radius, point.xml:28):
+// fl(sqrt(x)) - 0.7 > 0  <=>  x > kPointFarD2 (tests/test_utils_cpu.py checks it).
+constexpr double kPointFarD2 = 0.49;
 
 // 1/d for d > 0 in the normal range: v_rcp_f64 + one Newton-Raphson
 // refinement (3 dependent instructions instead of the 10 of the IEEE division
@@ -387,10 +390,23 @@ __device__ __forceinline__ int collide_in_frame(const PointModel& pm, const uint
   OGBX_WSTAT(12, slow);
 #ifndef OGBX_DIAG_BRANCHY
   {  // vertical-edge contact of the diagonal box, straight-line (no divergent branch)
+#ifdef OGBX_DIAG_SQRT
     const double dd = sqrt(cD ? d2D : 1.0);
     const double inv = fast_recip(dd);
     const bool far = dd - r > 0.0;
     slow = slow || (cD && !far && dd <= kMinVal);
+#else
+    // The contact test fl(sqrt(d2)) - r > 0 is decided exactly on d2 (far_d2 is
+    // the largest double whose correctly rounded root is <= r), so the flag is
+    // the oracle's bit for bit; the distance and the normal come from v_rsq_f64
+    // + one Newton-Raphson step (~1e-14 relative, the contact tolerance is 1e-9).
+    const double d2 = cD ? fmax(d2D, 1e-300) : 1.0;
+    const double y0 = __builtin_amdgcn_rsq(d2);
+    const double inv = y0 * fma(-0.5 * d2 * y0, y0, 1.5);
+    const double dd = d2 * inv;
+    const bool far = pm.radius == 0.7 ? d2 > kPointFarD2 : sqrt(d2) - r > 0.0;
+    slow = slow || (cD && !far && d2 <= kMinVal * kMinVal);
+#endif
     cD = cD && !far;
     dD = cD ? dd : 0.0;
     nDx = cD ? -tDx * inv : 0.0;
