@@ -17,4 +17,3 @@ def test_name_grammar_matches_reference(case):
     assert env_name == case['env_name']
     assert file_name == case['file_name']
     assert (mode == 'oraclerep') == (case['env_kwargs'] == {'use_oracle_rep': True})
-
