@@ -7,14 +7,20 @@ A step = one ``env.step(action)`` of all envs of this rank: one launch of
 ``maze_step_kernel`` through the C-ABI (Python -> ctypes -> libogbx), with the
 [N,2] float32 actions already resident in HBM (pre-generated ring, seed 1) and
 same-step auto-reset.  Timed region: barrier + synchronize, K steps, barrier +
-synchronize; the max over ranks is reported.  Multi-GPU: one process per GPU,
-each rank owns its own 65536 envs (independent shards, no data-path
-collective) -> "scaling": "weak"; ``value`` = envs x steps of all ranks / time.
+synchronize; the max over ranks is reported.
+
+Multi-GPU (the metric: N = 65,536 envs in total on 1/2/4/8 GPUs): one process
+per GPU; env i lives on rank i // (N/G) (``ogbench_amd.sharding``), each rank's
+handle is created at its global ``env_base`` with the one shared seed, so the
+G-rank job is the single-GPU job bit for bit (tests/test_shard_gpu.py).  No
+data-path collective; ``value`` = N x steps / time -> "scaling": "strong".
+The weak-scaling rate (65,536 envs per GPU) is reported in ``extra``.
 
 Extra fields (not ``value``): the same workload replayed from a hipGraph and
 as K fused steps per launch; ``roofline`` of maze_step_kernel (algorithmic
-87 B per env-step, DESIGN.md) from per-launch HIP events on the launch stream;
-``cpu_baseline`` = the oracle C restatement (OpenMP) on a bounded sample.
+87 B per env-step) from the median of >= 1000 per-launch HIP event
+pairs on the launch stream; ``cpu_baseline`` = the oracle C restatement
+(OpenMP) on a bounded sample.
 """
 
 import argparse
@@ -100,40 +106,49 @@ def _per_launch_ms(fn, launches, dev, host_us=120.0):
     return a.elapsed_time(b) / launches
 
 
-def _traffic(kernel, kern_ms, workload=None):
+def _median_launch_ms(fn, launches, dev, host_us=60.0):
+    """Median device duration of one launch: a HIP event pair on
+    the launch stream (torch's current stream, which libogbx launches on)
+    around each of `launches` launches.  A spin kernel queued first holds the
+    stream until the host has enqueued everything, so the launches run back to
+    back and each pair spans one kernel (plus its dispatch), not host time."""
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    torch.cuda.synchronize(dev)
+    torch.cuda._sleep(int(launches * host_us * 1e-6 * 2.4e9))
+    for i, (a, b) in enumerate(ev):
+        a.record(stream)
+        fn(i)
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
+
+
+def _traffic(kernel, workload, units, world):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/traffic.json, written by scripts/prof_summary.py from separate
-    FETCH_SIZE and WRITE_SIZE passes of this same command: bytes = (2 x FETCH_SIZE
-    + WRITE_SIZE) x 1024, the gfx950 correction of MI355X_MICROARCH.md section HBM).
-    None when no summary for this kernel is committed."""
+    FETCH_SIZE and WRITE_SIZE passes: bytes = (2 x FETCH_SIZE + WRITE_SIZE) x
+    1024, the gfx950 correction of MI355X_MICROARCH.md section HBM).  Only a
+    record of the same workload, per-launch units (envs or samples) and world
+    size counts; otherwise None (no PMC pass of this configuration)."""
     path = os.path.join(ROOT, 'profiles', 'traffic.json')
     try:
         with open(path) as f:
-            rec = json.load(f).get(kernel)
+            rec = json.load(f).get(f'{kernel}@{workload}')
     except (OSError, ValueError):
         return None
-    if workload is not None:
-        try:
-            with open(path) as f:
-                rec = json.load(f).get(f'{kernel}@{workload}', rec)
-        except (OSError, ValueError):
-            pass
-    if not rec:
+    if not rec or rec.get('units') != units or rec.get('world', 1) != world:
         return None
     return rec.get('hbm_bytes_per_launch')
 
 
 def bench_pointmaze(args, world, rank, dev):
-    import ogbench_amd
+    from ogbench_amd.sharding import shard
 
-    n = args.num_envs
-    env = ogbench_amd.make('pointmaze-large-v0', num_envs=n, device=dev, auto_reset=True)
-    task = (torch.arange(n, dtype=torch.int32, device=dev) % 5) + 1
-    env.reset(seed=rank, options=dict(task_id=task))
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1 + 1000 * rank)
+    total = args.num_envs
+    base, n = shard(total, world, rank)
     ring = args.ring
-    actions = torch.rand(ring, n, 2, device=dev, generator=gen, dtype=torch.float32) * 2 - 1
+    env, actions = _maze_job(total, base, n, ring, dev)
 
     def step(i):
         env.step(actions[i % ring])
@@ -141,18 +156,20 @@ def bench_pointmaze(args, world, rank, dev):
     for i in range(args.warmup):
         step(i)
     dt = _timed(step, args.steps, world, dev)
-    total_env_steps = n * args.steps * world
-    value = total_env_steps / dt
+    value = total * args.steps / dt
     ms_per_step = dt / args.steps * 1e3
 
     # kernel duration for the roofline (same workload, untimed pass)
-    kern_ms = _per_launch_ms(step, min(args.steps, 200), dev)
+    kern_ms = _median_launch_ms(step, max(1000, min(args.steps, 2000)), dev)
     alg_bytes = 87 * n  # 87 B per env-step
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
-    extra = {'eval_allgather': _eval_allgather(env, actions, world, dev)}
+    extra = {}
     if args.no_extras:
-        return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
+        return _finish_pointmaze(args, world, rank, total, n, value, ms_per_step, kern_ms, alg_bytes, achieved,
+                                 extra, env)
+    extra['eval_allgather'] = _eval_allgather(env, world, dev)
+    env.reset(seed=0, options=dict(task_id=(torch.arange(base, base + n, dtype=torch.int32, device=dev) % 5) + 1))
     # hipGraph replay of G steps (launch-bound inner loop captured once)
     try:
         G = 32
@@ -170,7 +187,7 @@ def bench_pointmaze(args, world, rank, dev):
             graph.replay()
         reps = max(1, args.steps // G)
         gdt = _timed(lambda i: graph.replay(), reps, world, dev)
-        extra['graph_replay_steps_per_s'] = n * G * reps * world / gdt
+        extra['graph_replay_steps_per_s'] = total * G * reps / gdt
     except Exception as e:  # pragma: no cover - reported, not fatal
         extra['graph_replay_error'] = repr(e)[:200]
     # K fused steps per launch (K = 1 and K = 100)
@@ -185,39 +202,68 @@ def bench_pointmaze(args, world, rank, dev):
     fused(0)
     reps = max(1, args.steps // K)
     fdt = _timed(fused, reps, world, dev)
-    extra[f'fused_k{K}_steps_per_s'] = n * K * reps * world / fdt
-    fk_ms = _per_launch_ms(fused, 5, dev)
+    extra[f'fused_k{K}_steps_per_s'] = total * K * reps / fdt
+    fk_ms = _median_launch_ms(fused, 20, dev)
     fused_bytes = (8 + 16 + 4 + 3) * n * K + (16 + 16 + 4 + 4 + 16 + 4 + 4) * n
     extra[f'fused_k{K}_kernel_ms'] = fk_ms
     extra[f'fused_k{K}_achieved_GBs'] = fused_bytes / (fk_ms * 1e-3) / 1e9
     if world > 1:
-        # strong scaling beside the weak-scaling value: N = 65,536 envs in total,
-        # n / world per rank (SURVEY section 8e reports both)
-        sn = max(64, n // world)
-        senv = ogbench_amd.make('pointmaze-large-v0', num_envs=sn, device=dev, auto_reset=True)
-        senv.reset(seed=rank, options=dict(task_id=task[:sn]))
-        sact = actions[:, :sn].contiguous()
+        # weak scaling beside the strong-scaling value: 65,536 envs per GPU
+        wn = 65536
+        wenv, wact = _maze_job(wn * world, rank * wn, wn, ring, dev)
         for i in range(args.warmup):
-            senv.step(sact[i % ring])
-        sdt = _timed(lambda i: senv.step(sact[i % ring]), args.steps, world, dev)
-        extra['strong_total_envs'] = sn * world
-        extra['strong_env_steps_per_s'] = sn * args.steps * world / sdt
-        senv.close()
-    return _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env)
+            wenv.step(wact[i % ring])
+        wdt = _timed(lambda i: wenv.step(wact[i % ring]), args.steps, world, dev)
+        extra['weak_envs_per_gpu'] = wn
+        extra['weak_total_envs'] = wn * world
+        extra['weak_env_steps_per_s'] = wn * world * args.steps / wdt
+        wenv.close()
+    return _finish_pointmaze(args, world, rank, total, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra,
+                             env)
 
 
-def _eval_allgather(env, actions, world, dev, steps=1000):
-    """Untimed: the eval success reduction of SURVEY section 8e -- per-task
-    {success, episodes} counters accumulated on the device for `steps` steps
-    (1000 = the TimeLimit, so every env completes at least one episode),
-    then all-gathered over the process group (RCCL over xGMI at N>1)."""
+def _maze_job(total, base, n, ring, dev, maze='large'):
+    """This rank's block [base, base+n) of a `total`-env pointmaze job: the
+    handle at its global env_base, reset with the shared seed 0 and task i%5+1
+    (global i), and its slice of the global action ring (seed 1, generated in
+    8192-env blocks so that a rank never holds the whole ring)."""
+    import ogbench_amd
+
+    env = ogbench_amd.make(f'pointmaze-{maze}-v0', num_envs=n, device=dev, auto_reset=True, env_base=base)
+    task = (torch.arange(base, base + n, dtype=torch.int32, device=dev) % 5) + 1
+    env.reset(seed=0, options=dict(task_id=task))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    acts = torch.empty(ring, n, 2, device=dev, dtype=torch.float32)
+    chunk = 8192
+    for c0 in range(0, total, chunk):
+        c1 = min(total, c0 + chunk)
+        blk = torch.rand(ring, c1 - c0, 2, device=dev, generator=gen, dtype=torch.float32) * 2 - 1
+        lo, hi = max(c0, base), min(c1, base + n)
+        if lo < hi:
+            acts[:, lo - base:hi - base] = blk[:, lo - c0:hi - c0]
+    return env, acts
+
+
+def _eval_allgather(env, world, dev, steps=1000):
+    """Untimed: the eval success reduction of SURVEY section 8e.  Every env
+    runs one episode of its task (i%5+1, global i) driven by the on-device
+    point expert (BFS oracle subgoal + N(0, 0.2) noise, generate_locomaze.py:
+    147-166); per-task {success, episodes} counters accumulate on the device
+    over `steps` steps (1000 = the TimeLimit, so every env finishes its
+    episode) and are all-gathered over the process group (RCCL over xGMI at
+    N>1)."""
     from ogbench_amd.evaluation import accumulate, env_task_ids, gather_counters, summarize
 
+    n, base = env.num_envs, env.env_base
+    env.reset(seed=0, options=dict(task_id=(torch.arange(base, base + n, dtype=torch.int32, device=dev) % 5) + 1))
     counters = torch.zeros(env.num_tasks, 2, dtype=torch.int64, device=dev)
-    remaining = torch.full((env.num_envs,), 1 << 30, dtype=torch.int32, device=dev)
+    remaining = torch.ones((n,), dtype=torch.int32, device=dev)
     tid = env_task_ids(env)
+    act = None
     for i in range(steps):
-        _, _, term, trunc, info = env.step(actions[i % actions.shape[0]])
+        act = env.expert_action(noise=0.2, seed=0, out=act)
+        _, _, term, trunc, info = env.step(act)
         accumulate(counters, info['success'].view(torch.uint8), term.view(torch.uint8), trunc.view(torch.uint8),
                    tid, remaining)
     _barrier(world)
@@ -227,8 +273,9 @@ def _eval_allgather(env, actions, world, dev, steps=1000):
     torch.cuda.synchronize(dev)
     ms = (time.perf_counter() - t0) * 1e3
     m = summarize(total, env.task_infos)
-    res = dict(episodes=int(total[:, 1].sum()), ranks=int(per_rank.shape[0]),
-               overall_success=m.get('evaluation/overall_success'), allgather_ms=ms)
+    res = dict(episodes=int(total[:, 1].sum()), ranks=int(per_rank.shape[0]), policy='expert (noise 0.2)',
+               overall_success=m.get('evaluation/overall_success'), allgather_ms=ms,
+               per_task={k.split('/')[1]: v for k, v in m.items() if k != 'evaluation/overall_success'})
     if world > 1:
         res.update(_cabi_allgather_check(counters, per_rank, world, dev))
     return res
@@ -262,7 +309,7 @@ def _cabi_allgather_check(counters, per_rank, world, dev):
         return {'cabi_allgather_error': repr(e)[:200]}
 
 
-def _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env):
+def _finish_pointmaze(args, world, rank, total, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env):
     result = dict(
         metric='env steps/sec at N=65536 parallel envs, pointmaze-large, 1/2/4/8 MI355X',
         value=value,
@@ -272,27 +319,31 @@ def _finish_pointmaze(args, world, rank, n, value, ms_per_step, kern_ms, alg_byt
         warmup=args.warmup,
         ms_per_step=ms_per_step,
         higher_is_better=True,
-        scaling='weak',
+        scaling='strong',
         vs_baseline=None,
         dtype='f64',
         data='synthetic (uniform [-1,1] float32 actions, Philox reset noise; no dataset)',
         config=dict(
             workload='pointmaze-large-navigate-v0',
+            total_envs=total,
             num_envs_per_gpu=n,
-            total_envs=n * world,
             auto_reset=True,
             task_id='i%5+1',
-            parallelism=f'env-shard x{world}',
+            seed=0,
+            parallelism=f'env-shard x{world} (contiguous blocks, global env_base)',
         ),
         roofline=dict(
-            bound='hbm',
+            # one wave's fp64 contact chain sets the launch time,
+            # not HBM: achieved/peak are still the HBM figures of 87 B/env-step
+            bound='latency',
             kernel='maze_step_kernel',
             achieved=achieved,
             peak=HBM_PEAK_GBS,
             unit='GB/s',
             frac=achieved / HBM_PEAK_GBS,
-            traffic=_traffic('maze_step_kernel', kern_ms),
+            traffic=_traffic('maze_step_kernel', 'pointmaze', n, world),
             kernel_ms=kern_ms,
+            kernel_ms_method='median of >= 1000 per-launch HIP event pairs',
             alg_bytes_per_launch=alg_bytes,
         ),
         extra=extra,
@@ -326,6 +377,67 @@ def cpu_baseline_pointmaze(n, args):
         kind='port',
         sample=f'{steps} steps x {n} envs of pointmaze-large with auto-reset ({dt:.1f} s)',
     )
+
+
+def bench_pointmaze_n1(args, world, rank, dev):
+    """pointmaze-medium-navigate-v0 with ONE env (BASELINE configs[0]; SURVEY 8d
+    row 1: plumbing).  A step = one Gymnasium-surface ``env.step(action)`` of
+    the single env through the C-ABI (one launch), actions U[-1,1]^2 float32
+    from torch.Generator(seed=0) resident on the device, task round robin
+    1..5 per episode via same-step auto-reset (TimeLimit 1000).  The number is
+    launch-latency bound by construction (one env); ``cpu_baseline`` is the
+    oracle C restatement stepping the same single env on 1 core (the
+    reference MuJoCo step cannot run here: MuJoCo is absent)."""
+    import ogbench_amd
+
+    env = ogbench_amd.make('pointmaze-medium-v0', num_envs=1, device=dev, auto_reset=True)
+    env.reset(seed=rank, options=dict(task_id=1))
+    ring = 1000
+    gen = torch.Generator(device='cpu').manual_seed(0)
+    actions = (torch.rand(ring, 1, 2, generator=gen) * 2 - 1).float().to(dev)
+
+    def step(i):
+        env.step(actions[i % ring])
+
+    for i in range(args.warmup):
+        step(i)
+    dt = _timed(step, args.steps, world, dev)
+    kern_ms = _median_launch_ms(step, 1000, dev)
+    result = dict(
+        metric='env steps/sec, pointmaze-medium-navigate-v0, N=1 env (Gymnasium surface)',
+        value=args.steps * world / dt, unit='env_steps/s', n_gpus=world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=dt / args.steps * 1e3, higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f64',
+        data='synthetic (U[-1,1]^2 float32 actions, torch.Generator seed 0; Philox reset noise)',
+        config=dict(workload='pointmaze-medium-navigate-v0 N=1', num_envs_per_gpu=1, auto_reset=True,
+                    parallelism=f'replica x{world}'),
+        roofline=dict(bound='latency', kernel='maze_step_kernel', achieved=87 / (kern_ms * 1e-3) / 1e9,
+                      peak=HBM_PEAK_GBS, unit='GB/s', frac=87 / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      traffic=None, kernel_ms=kern_ms, alg_bytes_per_launch=87),
+        extra={},
+    )
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline_pointmaze_n1(args)
+    env.close()
+    return result
+
+
+def cpu_baseline_pointmaze_n1(args):
+    """The oracle C restatement stepping one pointmaze-medium env per call
+    (kind 'port', 1 core), as a Gymnasium loop would; auto-reset with Philox."""
+    from oracle import locomaze as orc
+
+    rng = np.random.RandomState(0)
+    st = orc.reset('medium', np.array([1], np.int32), orc.reset_draws(1, 0))
+    key = orc.philox_key(0, orc.TAG_MAZE_RESET)
+    acts = rng.uniform(-1, 1, (1000, 1, 1, 2)).astype(np.float32)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < min(args.cpu_seconds, 5.0):
+        for i in range(1000):
+            orc.step('medium', st, acts[i], auto_reset=1, key=key, nthreads=1)
+        steps += 1000
+    dt = time.perf_counter() - t0
+    return dict(value=steps / dt, unit='env_steps/s', cores=1, kind='port',
+                sample=f'{steps} single-env steps of pointmaze-medium through the ctypes oracle ({dt:.1f} s)')
 
 
 def bench_gcsample(args, world, rank, dev):
@@ -365,7 +477,7 @@ def bench_gcsample(args, world, rank, dev):
         step(i)
     dt = _timed(step, args.steps, world, dev)
     value = B * args.steps * world / dt
-    kern_ms = _per_launch_ms(step, min(args.steps, 200), dev)
+    kern_ms = _median_launch_ms(step, 1000, dev)
     per_sample = 2424  # algorithmic bytes per sample (humanoid layout)
     achieved = per_sample * B / (kern_ms * 1e-3) / 1e9
     NB = 256
@@ -391,7 +503,7 @@ def bench_gcsample(args, world, rank, dev):
         config=dict(workload='humanoidmaze-large-navigate-v0 offline replay', rows=R, batch=B,
                     agent_config='gciql humanoid (discount 0.995)', parallelism=f'replica x{world}'),
         roofline=dict(bound='hbm', kernel='gc_sample_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('gc_sample_kernel', kern_ms), kernel_ms=kern_ms,
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('gc_sample_kernel', 'gcsample', B, world), kernel_ms=kern_ms,
                       alg_bytes_per_launch=per_sample * B),
         extra=extra,
     )
@@ -431,7 +543,7 @@ def bench_hgcsample(args, world, rank, dev):
     for i in range(args.warmup):
         step(i)
     dt = _timed(step, args.steps, world, dev)
-    kern_ms = _per_launch_ms(step, min(args.steps, 200), dev)
+    kern_ms = _median_launch_ms(step, 1000, dev)
     # 12 gathered 276-B observation rows + actions 84 + terminals/valids 8,
     # read and written, + valid_idxs/traj_end lookups 16 + 9 x 8-B scalars written
     per_sample = 2 * (12 * 276 + 84 + 8) + 16 + 72
@@ -458,7 +570,7 @@ def bench_hgcsample(args, world, rank, dev):
                     agent_config='hiql humanoid (discount 0.995, subgoal_steps 100)',
                     parallelism=f'replica x{world}'),
         roofline=dict(bound='hbm', kernel='hgc_sample_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('hgc_sample_kernel', kern_ms),
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('hgc_sample_kernel', 'hgcsample', B, world),
                       kernel_ms=kern_ms, alg_bytes_per_launch=per_sample * B),
         extra=extra,
     )
@@ -552,6 +664,8 @@ def bench_powder(args, world, rank, dev, level='easy'):
     steps = args.steps - args.steps % 3 if args.steps >= 3 else args.steps
     dt = _timed(step, steps, world, dev)
     value = n * steps * world / dt
+    # mean over whole 3-step action cycles (the forward runs on one step in
+    # three, so a per-launch median would pick a render-only step)
     kern_ms = _per_launch_ms(step, min(steps, 201) - min(steps, 201) % 3 or 1, dev)
     # algorithmic bytes per env-step: obs write H*W*6, world read H*W, world
     # write H*W on one step in three, action 4, reward 4, flags 3, ctrl 16.
@@ -585,7 +699,7 @@ def bench_powder(args, world, rank, dev, level='easy'):
         config=dict(workload=f'powderworld-{level}-v0 world_size=64', num_envs_per_gpu=n, auto_reset=True,
                     parallelism=f'env-shard x{world}'),
         roofline=dict(bound='hbm', kernel=kern, achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic(kern, kern_ms, args.workload), kernel_ms=kern_ms,
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic(kern, args.workload, n, world), kernel_ms=kern_ms,
                       alg_bytes_per_launch=per_step * n),
         extra=extra,
     )
@@ -652,7 +766,8 @@ def main():
     ap.add_argument('--steps', type=int, default=2000)
     ap.add_argument('--warmup', type=int, default=100)
     ap.add_argument('--workload', default='pointmaze',
-                    choices=['pointmaze', 'powder', 'powder-medium', 'powder-hard', 'gcsample', 'hgcsample'])
+                    choices=['pointmaze', 'pointmaze-medium-n1', 'powder', 'powder-medium', 'powder-hard', 'gcsample',
+                             'hgcsample'])
     ap.add_argument('--num-envs', type=int, default=65536)
     ap.add_argument('--ring', type=int, default=128)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -668,7 +783,7 @@ def main():
     import sys
 
     sys.path.insert(0, ROOT)
-    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, gcsample=bench_gcsample, hgcsample=bench_hgcsample,
+    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, **{'pointmaze-medium-n1': bench_pointmaze_n1}, gcsample=bench_gcsample, hgcsample=bench_hgcsample,
               **{'powder-medium': lambda *a: bench_powder(*a, level='medium'),
                  'powder-hard': lambda *a: bench_powder(*a, level='hard')})[args.workload]
     result = fn(args, world, rank, dev)

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define OGBX_ABI_VERSION 1
+#define OGBX_ABI_VERSION 2
 
 typedef enum {
   OGBX_OK = 0,
@@ -69,6 +69,13 @@ typedef struct {
   int32_t reward_task_id;    /* -1 = goal-conditioned (None); 0 => default task 1
                                 (maze.py:361-362); 1..num_tasks single-task. */
   int32_t max_episode_steps; /* TimeLimit, locomaze/__init__.py:20 (1000). */
+  int64_t env_base;          /* Global index of env 0 of this handle.  Every
+                                Philox stream (reset noise, task draws, teleport
+                                out-portal, expert noise, set_goal noise) is
+                                counted by the GLOBAL env index env_base + i, so
+                                G ranks holding envs [r*N/G, (r+1)*N/G) with one
+                                shared seed reproduce the single-GPU run of N
+                                envs bit for bit.  0 = unsharded. */
 } ogbx_maze_opts;
 
 /* Create a batch of `n_envs` maze envs on `device`.
@@ -374,6 +381,8 @@ typedef struct {
   int32_t num_elems;         /* 2 = easy, 5 = medium, 8 = hard (:57-62) */
   int32_t max_episode_steps; /* TimeLimit (500 in the registry) */
   int32_t pad;
+  int64_t env_base;          /* global index of env 0 (Philox counter; see
+                                ogbx_maze_opts.env_base) */
 } ogbx_powder_opts;
 
 /* PowderworldEnv.__init__ (+ set_tasks, :81-282).  Easy: the goal world of

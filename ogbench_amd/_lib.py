@@ -40,6 +40,7 @@ class MazeOpts(ctypes.Structure):
         ('add_noise_to_goal', c_int32),
         ('reward_task_id', c_int32),
         ('max_episode_steps', c_int32),
+        ('env_base', c_int64),
     ]
 
 
@@ -51,6 +52,7 @@ class PowderOpts(ctypes.Structure):
         ('num_elems', c_int32),
         ('max_episode_steps', c_int32),
         ('pad', c_int32),
+        ('env_base', c_int64),
     ]
 
 

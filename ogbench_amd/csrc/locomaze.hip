@@ -36,6 +36,7 @@ struct MazeParams {
   int32_t H, W, num_tasks, loco_type;
   int32_t success_pre, terminate_at_goal, add_noise_to_goal, reward_task_id;
   int32_t max_steps, n_tp_in, n_tp_out, pad_;
+  int64_t env_base;  // global index of env 0: Philox streams count global envs
   double goal_tol, tp_radius;
   double tp_in[2][2];
   double tp_out[3][2];
@@ -170,10 +171,11 @@ __global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __res
   if (i >= n) return;
   if (mask != nullptr && mask[i] == 0) return;
   uint32_t ep = S.episode[i] + 1u;
+  const uint64_t gi = (uint64_t)(i + P.env_base);
   int32_t task;
   if (P.reward_task_id > 0) task = P.reward_task_id;
   else if (task_id != nullptr) task = task_id[i];
-  else task = draw_task(P, (uint64_t)i, ep, k0, k1);
+  else task = draw_task(P, gi, ep, k0, k1);
   if (task < 1 || task > P.num_tasks) task = 1;  // validated on the host
   double r[4];
   if (noise != nullptr) {
@@ -182,7 +184,7 @@ __global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __res
     r[2] = noise[4 * i + 2];
     r[3] = noise[4 * i + 3];
   } else {
-    reset_draws((uint64_t)i, ep, k0, k1, r);
+    reset_draws(gi, ep, k0, k1, r);
   }
   double x, y, gx, gy;
   reset_one(P, task, task_xy ? task_xy + 4 * i : nullptr, r, x, y, gx, gy);
@@ -214,6 +216,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
   stage_nbmask(P, nb_s);
   const int64_t i = env_of_lane(epw);
   if (i < 0 || i >= n) return;
+  const uint64_t gi = (uint64_t)(i + P.env_base);
 
   double2 q = reinterpret_cast<const double2*>(S.qpos)[i];
   double2 g = reinterpret_cast<const double2*>(S.goal)[i];
@@ -221,6 +224,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
   int32_t task = S.task[i];
   uint32_t ep = S.episode[i];
   double x = q.x, y = q.y, gx = g.x, gy = g.y;
+  bool reset_any = false;  // goal / episode change only on an auto-reset
 
   for (int32_t k = 0; k < k_steps; ++k) {
     const int64_t o = (int64_t)k * n + i;
@@ -244,7 +248,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     if (P.n_tp_in > 0) {
       for (int t = 0; t < P.n_tp_in; ++t) {
         if (goal_reached(x, y, P.tp_in[t][0], P.tp_in[t][1], P.tp_radius * 1.5)) {
-          u32x4 c = philox4x32_10({(uint32_t)i, ep, 0x100u + (uint32_t)el, (uint32_t)(i >> 32)},
+          u32x4 c = philox4x32_10({(uint32_t)gi, ep, 0x100u + (uint32_t)el, (uint32_t)(gi >> 32)},
                                   k0 ^ kTagMazeTeleport, k1);
           int o_idx = (int)bounded_u32(c.x, (uint32_t)P.n_tp_out);
           x = P.tp_out[o_idx][0];
@@ -266,8 +270,9 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     if (auto_reset && (term || trunc)) {
       if (final_obs != nullptr) reinterpret_cast<double2*>(final_obs)[o] = make_double2(ox, oy);
       ep += 1u;
+      reset_any = true;
       double r[4];
-      reset_draws((uint64_t)i, ep, k0, k1, r);
+      reset_draws(gi, ep, k0, k1, r);
       reset_one(P, task, nullptr, r, x, y, gx, gy);
       el = 0;
       wx = x;
@@ -276,9 +281,11 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     reinterpret_cast<double2*>(obs)[o] = make_double2(wx, wy);
   }
   reinterpret_cast<double2*>(S.qpos)[i] = make_double2(x, y);
-  reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
   S.elapsed[i] = el;
-  S.episode[i] = ep;
+  if (reset_any) {
+    reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
+    S.episode[i] = ep;
+  }
 }
 
 template <bool kF64>
@@ -402,7 +409,8 @@ __global__ void expert_action_kernel(const MazeParams* __restrict__ Pp, const in
     nx = normal[2 * t];
     ny = normal[2 * t + 1];
   } else {
-    const u32x4 w = philox4x32_10({(uint32_t)t, call_lo, 0x45u, (uint32_t)(t >> 32) ^ call_hi}, k0, k1);
+    const uint64_t gt = (uint64_t)(t + P.env_base);
+    const u32x4 w = philox4x32_10({(uint32_t)gt, call_lo, 0x45u, (uint32_t)(gt >> 32) ^ call_hi}, k0, k1);
     const double u1 = 1.0 - u01_from(w.x, w.y);  // (0, 1]
     const double u2 = u01_from(w.z, w.w);
     const double r = sqrt(-2.0 * log(u1));
@@ -434,7 +442,8 @@ __global__ void set_goal_kernel(const MazeParams* __restrict__ Pp, MazeState S, 
       r0 = noise[2 * i];
       r1 = noise[2 * i + 1];
     } else {
-      const u32x4 w = philox4x32_10({(uint32_t)i, call_lo, 0x47u, (uint32_t)(i >> 32) ^ call_hi}, k0, k1);
+      const uint64_t gi = (uint64_t)(i + P.env_base);
+      const u32x4 w = philox4x32_10({(uint32_t)gi, call_lo, 0x47u, (uint32_t)(gi >> 32) ^ call_hi}, k0, k1);
       r0 = -1.0 + 2.0 * u01_from(w.x, w.y);
       r1 = -1.0 + 2.0 * u01_from(w.z, w.w);
     }
@@ -564,6 +573,7 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
   OGBX_CHECK(opts->success_timing == 0 || opts->success_timing == 1, OGBX_EINVAL,
              "success_timing must be 'pre' or 'post'");
   OGBX_CHECK(opts->max_episode_steps > 0, OGBX_EINVAL, "max_episode_steps must be positive");
+  OGBX_CHECK(opts->env_base >= 0, OGBX_EINVAL, "env_base must be >= 0");
   OGBX_CHECK(opts->reward_task_id <= spec->ntasks, OGBX_EINVAL,
              "Task ID must be in [1, " + std::to_string(spec->ntasks) + "].");
   ogbx_status st = use_device(device);
@@ -592,6 +602,7 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
   P.reward_task_id = opts->reward_task_id == 0 ? 1 : opts->reward_task_id;  // maze.py:361-362
   if (opts->reward_task_id < 0) P.reward_task_id = -1;
   P.max_steps = opts->max_episode_steps;
+  P.env_base = opts->env_base;
   P.goal_tol = opts->loco_type == 0 ? 1.0 : 0.5;  // maze.py:86
   for (int c = 0; c < spec->H * spec->W; ++c) P.wall[c] = spec->rows[c] == '1';
   for (int i = 0; i < spec->H; ++i)

@@ -78,6 +78,7 @@ struct PowderParams {
   uint32_t lut[32];              // render colour of each id, R | G<<8 | B<<16
   int32_t seq_len[kPwMaxTasks];  // goal replay sequences (elem idx, x, y)
   int8_t seq[kPwMaxTasks][kPwMaxSeq][3];
+  int64_t env_base;              // global index of env 0 of this handle (sharded runs)
 };
 
 struct PowderState {
@@ -402,20 +403,21 @@ __global__ void __launch_bounds__(256) pw_reset_kernel(const PowderParams* __res
   using G = Geo<WS>;
   __shared__ PwShared<WS> sh;
   const int64_t e = blockIdx.x;
+  const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
   if (mask != nullptr && mask[e] == 0) return;
   Blk<WS> b(sh);
   load_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, ne = Pp->num_elems, xy = Pp->xy_size, nt = Pp->num_tasks;
   const uint32_t ep = S.episode[e] + 1u;
-  int task = task_id ? task_id[e] : 1 + (int)pw_draw(e, ep, 0, k0, k1, (uint32_t)nt);
+  int task = task_id ? task_id[e] : 1 + (int)pw_draw(ge, ep, 0, k0, k1, (uint32_t)nt);
   if (task < 1 || task > nt) task = 1;
   int elem, x, y;
   if (reset_action) {
     elem = reset_action[3 * e], x = reset_action[3 * e + 1], y = reset_action[3 * e + 2];
   } else {
-    elem = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
-    x = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
-    y = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+    elem = (int)pw_draw(ge, ep, 1, k0, k1, (uint32_t)ne);
+    x = (int)pw_draw(ge, ep, 2, k0, k1, (uint32_t)xy);
+    y = (int)pw_draw(ge, ep, 3, k0, k1, (uint32_t)xy);
   }
   __syncthreads();  // tables
   typename Blk<WS>::S own = b.reset_world(sh.elem_ids[elem], x * grid, y * grid, brush);
@@ -448,6 +450,7 @@ __global__ void __launch_bounds__(256) pw_step_kernel(
   __shared__ PwShared<WS> sh;
   Blk<WS> b(sh);
   const int64_t e = blockIdx.x;
+  const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
   const int act0 = action[e];  // first step's action, loaded with the world (not after the barrier)
   load_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
@@ -468,7 +471,7 @@ __global__ void __launch_bounds__(256) pw_step_kernel(
     bool succ = (ctrl & kCtrlSuccess) != 0;
     auto rnd = [&](int bound) -> int {
       if (draws) return draws[o];
-      return (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)bound);
+      return (int)pw_draw(ge, ep, (uint32_t)el, a0, a1, (uint32_t)bound);
     };
     if (stage == 0) {
       elem = act >= 0 && act < ne ? act : rnd(ne);
@@ -491,9 +494,9 @@ __global__ void __launch_bounds__(256) pw_step_kernel(
     }
     if (auto_reset && (succ || trunc)) {
       ep += 1u;
-      const int re = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
-      const int rx = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
-      const int ry = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+      const int re = (int)pw_draw(ge, ep, 1, k0, k1, (uint32_t)ne);
+      const int rx = (int)pw_draw(ge, ep, 2, k0, k1, (uint32_t)xy);
+      const int ry = (int)pw_draw(ge, ep, 3, k0, k1, (uint32_t)xy);
       own = b.reset_world(sh.elem_ids[re], rx * grid, ry * grid, brush);
       __syncthreads();  // every thread is past its reads of `a`
       store_seg(sh.a + b.r * G::W + b.c0, own);
@@ -596,24 +599,25 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   constexpr int C = WS * WS;
   __shared__ PwFullShared<WS> sh;
   const int64_t e = blockIdx.x;
+  const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
   if (mask != nullptr && mask[e] == 0) return;
   FW<WS> fw(sh);
   pwf_tables(sh, Pp);
   const int ne = Pp->num_elems, xy = Pp->xy_size, nt = Pp->num_tasks;
   const uint32_t ep = S.episode[e] + 1u;
-  int task = task_id ? task_id[e] : 1 + (int)pw_draw(e, ep, 0, k0, k1, (uint32_t)nt);
+  int task = task_id ? task_id[e] : 1 + (int)pw_draw(ge, ep, 0, k0, k1, (uint32_t)nt);
   if (task < 1 || task > nt) task = 1;
   int elem, x, y;
   if (reset_action) {
     elem = reset_action[3 * e], x = reset_action[3 * e + 1], y = reset_action[3 * e + 2];
   } else {
-    elem = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
-    x = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
-    y = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+    elem = (int)pw_draw(ge, ep, 1, k0, k1, (uint32_t)ne);
+    x = (int)pw_draw(ge, ep, 2, k0, k1, (uint32_t)xy);
+    y = (int)pw_draw(ge, ep, 3, k0, k1, (uint32_t)xy);
   }
   const int len = Pp->seq_len[task - 1];
   for (int q = 0; q <= len; ++q)
-    pwf_reset_op(fw, Pp, task, q, elem, x, y, rand ? rand + (size_t)e * rand_rows * 3 * C : nullptr, r0, r1, e, ep,
+    pwf_reset_op(fw, Pp, task, q, elem, x, y, rand ? rand + (size_t)e * rand_rows * 3 * C : nullptr, r0, r1, ge, ep,
                  goal_obs + (size_t)e * C * 6);
 #pragma unroll
   for (int k = 0; k < FW<WS>::CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
@@ -640,6 +644,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   __shared__ PwFullShared<WS> sh;
   FW<WS> fw(sh);
   const int64_t e = blockIdx.x;
+  const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
   if (skip != nullptr && skip[e]) return;  // stepped by pwf_light_step_kernel
   pwf_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
@@ -663,7 +668,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     bool succ = (ctrl & kCtrlSuccess) != 0;
     auto rnd = [&](int bound) -> int {
       if (draws) return draws[o];
-      return (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)bound);
+      return (int)pw_draw(ge, ep, (uint32_t)el, a0, a1, (uint32_t)bound);
     };
     if (stage == 0) {
       elem = act >= 0 && act < ne ? act : rnd(ne);
@@ -692,9 +697,9 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
       if (auto_reset && (succ || trunc)) {
         reset = true;
         ep += 1u;
-        re = (int)pw_draw(e, ep, 1, k0, k1, (uint32_t)ne);
-        rx = (int)pw_draw(e, ep, 2, k0, k1, (uint32_t)xy);
-        ry = (int)pw_draw(e, ep, 3, k0, k1, (uint32_t)xy);
+        re = (int)pw_draw(ge, ep, 1, k0, k1, (uint32_t)ne);
+        rx = (int)pw_draw(ge, ep, 2, k0, k1, (uint32_t)xy);
+        ry = (int)pw_draw(ge, ep, 3, k0, k1, (uint32_t)xy);
         op_end = len;
       }
     };
@@ -702,13 +707,13 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     for (; op <= op_end; ++op) {
       fw.fence_idx();
       if (op < 0) {
-        fw.forward_rand(rand ? rand + (size_t)o * 3 * C : nullptr, r0, r1, e, ep, kRandStep | el_step);
+        fw.forward_rand(rand ? rand + (size_t)o * 3 * C : nullptr, r0, r1, ge, ep, kRandStep | el_step);
         fw.paint(sh.elem_ids[elem], x * grid, y * grid, brush);
         succ = fw.errors() < tol;
         dirty = true;
         finish_step();
       } else {
-        pwf_reset_op(fw, Pp, task, op, re, rx, ry, nullptr, r0, r1, e, ep, nullptr);
+        pwf_reset_op(fw, Pp, task, op, re, rx, ry, nullptr, r0, r1, ge, ep, nullptr);
       }
     }
     if (reset) {
@@ -753,6 +758,7 @@ __global__ void __launch_bounds__(256) pwf_light_step_kernel(
   __shared__ alignas(16) uint16_t st[C * 3];  // 6 observation bytes per cell
   __shared__ uint32_t lut[32];
   const int64_t e = blockIdx.x;
+  const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
   const int t = threadIdx.x;
   if (t < 32) lut[t] = Pp->lut[t];
   const int ctrl = S.ctrl[e];
@@ -766,10 +772,10 @@ __global__ void __launch_bounds__(256) pwf_light_step_kernel(
   const int act = action[e];
   if (stage == 0) {
     const int ne = Pp->num_elems;
-    elem = act >= 0 && act < ne ? act : (draws ? draws[e] : (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)ne));
+    elem = act >= 0 && act < ne ? act : (draws ? draws[e] : (int)pw_draw(ge, ep, (uint32_t)el, a0, a1, (uint32_t)ne));
   } else {
     const int xy = Pp->xy_size;
-    x = act >= 0 && act < xy ? act : (draws ? draws[e] : (int)pw_draw(e, ep, (uint32_t)el, a0, a1, (uint32_t)xy));
+    x = act >= 0 && act < xy ? act : (draws ? draws[e] : (int)pw_draw(ge, ep, (uint32_t)el, a0, a1, (uint32_t)xy));
   }
   stage += 1;
   el += 1;
@@ -1094,6 +1100,7 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
   OGBX_CHECK(opts->grid_size == 4 && opts->brush_size == 4, OGBX_EINVAL,
              "only the registered grid_size=4 / brush_size=4 are supported");
   OGBX_CHECK(opts->max_episode_steps > 0, OGBX_EINVAL, "max_episode_steps must be positive");
+  OGBX_CHECK(opts->env_base >= 0, OGBX_EINVAL, "env_base must be >= 0");
   ogbx_status st = use_device(device);
   if (st != OGBX_OK) return st;
   auto* e = new ogbx_powder_env();
@@ -1111,6 +1118,7 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
   static const int ids2[2] = {8, 9}, ids8[8] = {2, 3, 7, 8, 9, 4, 5, 6};
   for (int k = 0; k < ne; ++k) P.elem_ids[k] = ne == 2 ? ids2[k] : ids8[k];
   P.max_steps = opts->max_episode_steps;
+  P.env_base = opts->env_base;
   // render LUT: uint8(clip(float32(c)/255 * 1 + 0) * 255) (sim.py:402-453)
   static const int colors[21][3] = {
       {236, 240, 241}, {108, 122, 137}, {243, 194, 58}, {75, 119, 190}, {179, 157, 219},

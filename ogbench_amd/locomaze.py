@@ -85,7 +85,11 @@ class MazeEnv:
         max_episode_steps=1000,
         auto_reset=False,
         seed=None,
+        env_base=0,
     ):
+        """env_base: global index of env 0 of this batch.  Every Philox stream
+        is counted by the global env index, so G shards [r*N/G, (r+1)*N/G) with
+        the same seed reproduce one batch of N envs bit for bit."""
         if loco_env_type not in LOCO_TYPES:
             raise ValueError(f'Unknown locomotion environment type: {loco_env_type}')
         if maze_type not in MAZE_TYPES:
@@ -123,7 +127,9 @@ class MazeEnv:
             add_noise_to_goal=int(bool(add_noise_to_goal)),
             reward_task_id=-1 if reward_task_id is None else int(reward_task_id),
             max_episode_steps=self.max_episode_steps,
+            env_base=int(env_base),
         )
+        self.env_base = int(env_base)
         L = _lib.lib()
         h = _lib.c_void_p()
         with torch.cuda.device(self.device):

@@ -56,6 +56,7 @@ class PowderworldEnv:
         max_episode_steps=500,
         auto_reset=False,
         seed=None,
+        env_base=0,
     ):
         assert mode in ('task', 'data'), 'mode must be task or data'
         if mode != 'task':
@@ -80,7 +81,9 @@ class PowderworldEnv:
             brush_size=self._brush_size,
             num_elems=self._num_elems,
             max_episode_steps=self.max_episode_steps,
+            env_base=int(env_base),
         )
+        self.env_base = int(env_base)
         L = _lib.lib()
         h = _lib.c_void_p()
         with torch.cuda.device(self.device):

@@ -94,8 +94,9 @@ def reset(maze, task_id, noise, **opts):
     return st
 
 
-def step(maze, st, actions, auto_reset=0, key=(0, 0), nthreads=1):
-    """k steps (actions [k,n,2]) of the env-level oracle; st is updated in place."""
+def step(maze, st, actions, auto_reset=0, key=(0, 0), nthreads=1, env_base=0):
+    """k steps (actions [k,n,2]) of the env-level oracle; st is updated in place.
+    env_base: global index of env 0 (Philox counter of the auto-reset draws)."""
     a = np.ascontiguousarray(actions)
     k, n = a.shape[0], a.shape[1]
     out = dict(obs=np.zeros((k, n, 2)), reward=np.zeros((k, n), np.float32),
@@ -105,7 +106,17 @@ def step(maze, st, actions, auto_reset=0, key=(0, 0), nthreads=1):
                         _p(st['task']), _p(st['episode']), ctypes.c_int64(n), _p(a), int(a.dtype == np.float64),
                         int(k), _p(out['obs']), _p(out['reward']), _p(out['terminated']), _p(out['truncated']),
                         _p(out['success']), int(auto_reset), ctypes.c_uint32(key[0]), ctypes.c_uint32(key[1]),
-                        int(nthreads))
+                        int(nthreads), ctypes.c_int64(env_base))
+    return out
+
+
+def reset_draws(n, seed, env_base=0, episode=1):
+    """The Philox uniform(-1,1) reset draws [n,4] libogbx uses for a reset with
+    `seed` of envs env_base..env_base+n-1 (episode counter after the reset)."""
+    k0, k1 = philox_key(seed, TAG_MAZE_RESET)
+    out = np.zeros((n, 4))
+    lib().orc_reset_draws(ctypes.c_int64(n), ctypes.c_int64(env_base), ctypes.c_uint32(episode), ctypes.c_uint32(k0),
+                          ctypes.c_uint32(k1), _p(out))
     return out
 
 

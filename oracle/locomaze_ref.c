@@ -351,6 +351,12 @@ static void reset_draws(uint64_t i, uint32_t ep, uint32_t k0, uint32_t k1, doubl
   r[3] = -1.0 + 2.0 * u53(b[2], b[3]);
 }
 
+/* The reset draws [n,4] that libogbx's maze_reset_kernel uses for envs
+ * env_base .. env_base+n-1 at episode counter ep (checker of Philox resets). */
+void orc_reset_draws(int64_t n, int64_t env_base, uint32_t ep, uint32_t k0, uint32_t k1, double* out) {
+  for (int64_t i = 0; i < n; ++i) reset_draws((uint64_t)(env_base + i), ep, k0, k1, out + 4 * i);
+}
+
 /* ------------------------------------------------------------- env level */
 typedef struct {
   int success_pre, terminate_at_goal, add_noise_to_goal, reward_task_id, max_steps;
@@ -411,12 +417,13 @@ int orc_maze_reset(const char* maze, const int* opts_i, const int32_t* task_id,
 /* k_steps of TimeLimit(MazeEnv(PointEnv)).step for n envs, host state in/out.
  * opts_i = {success_pre, terminate_at_goal, add_noise_to_goal, reward_task_id,
  *           max_steps, is_not_point}.  Auto-reset draws come from Philox with
- * key (k0, k1) and the per-env episode counter, exactly like libogbx. */
+ * key (k0, k1), the GLOBAL env index env_base + i and the per-env episode
+ * counter, exactly like libogbx (ogbx_maze_opts.env_base). */
 int orc_maze_step(const char* maze, const int* opts_i, double* qpos, double* goal,
                   int32_t* elapsed, const int32_t* task, uint32_t* episode, int64_t n,
                   const void* action, int act_f64, int k_steps, double* obs, float* reward,
                   uint8_t* term, uint8_t* trunc, uint8_t* succ, int auto_reset, uint32_t k0,
-                  uint32_t k1, int nthreads) {
+                  uint32_t k1, int nthreads, int64_t env_base) {
   const orc_maze* mz = find_maze(maze);
   if (!mz) return -1;
   orc_consts C = consts();
@@ -460,7 +467,8 @@ int orc_maze_step(const char* maze, const int* opts_i, double* qpos, double* goa
           double px, py;
           ij_to_xy(tin[t][0], tin[t][1], &px, &py);
           if (success_of(x, y, px, py, 1.0 * 1.5)) {
-            uint32_t c[4] = {(uint32_t)i, ep, 0x100u + (uint32_t)el, (uint32_t)((uint64_t)i >> 32)};
+            const uint64_t gi = (uint64_t)(env_base + i);
+            uint32_t c[4] = {(uint32_t)gi, ep, 0x100u + (uint32_t)el, (uint32_t)(gi >> 32)};
             philox(c, k0 ^ 0x4D5A0002u, k1);
             const int oidx = (int)(((uint64_t)c[0] * 3u) >> 32);
             ij_to_xy(tout[oidx][0], tout[oidx][1], &x, &y);
@@ -480,7 +488,7 @@ int orc_maze_step(const char* maze, const int* opts_i, double* qpos, double* goa
       if (auto_reset && (te || tr)) {
         double r[4];
         ep += 1u;
-        reset_draws((uint64_t)i, ep, k0, k1, r);
+        reset_draws((uint64_t)(env_base + i), ep, k0, k1, r);
         reset_env(mz, &o, task[i], r, &x, &y, &gx, &gy);
         el = 0;
       }

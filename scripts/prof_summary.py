@@ -11,7 +11,7 @@ the entry of the workload's dominant kernel in profiles/traffic.json:
   that kernel's dispatches (FETCH_SIZE/WRITE_SIZE in KiB; FETCH_SIZE doubled per
   the gfx950 note in MI355X_MICROARCH.md section HBM).
 
-  python scripts/prof_summary.py --round r01 --workload powder --kernel pw_step_kernel
+  python scripts/prof_summary.py --round r02 --workload powder --kernel pw_step_kernel --units 4096
 """
 
 import argparse
@@ -50,6 +50,8 @@ def main():
     ap.add_argument('--round', required=True)
     ap.add_argument('--workload', required=True)
     ap.add_argument('--kernel', required=True)
+    ap.add_argument('--units', type=int, required=True, help='envs or samples per launch of the profiled run')
+    ap.add_argument('--world', type=int, default=1)
     ap.add_argument('--out', default=os.path.join(ROOT, 'gpurun_out'))
     a = ap.parse_args()
     stats = _one(os.path.join(a.out, f'prof_{a.workload}', '**', '*kernel_stats.csv'))
@@ -81,14 +83,16 @@ def main():
         kernel_trace_avg_ns=avg_ns,
         kernel_trace_calls=calls,
         stats_file=os.path.relpath(dst, ROOT),
+        units=a.units,
+        world=a.world,
     )
     tpath = os.path.join(ROOT, 'profiles', 'traffic.json')
     data = {}
     if os.path.exists(tpath):
         with open(tpath) as f:
             data = json.load(f)
-    data[a.kernel] = rec
-    data[f'{a.kernel}@{a.workload}'] = rec  # kernels shared by several workloads (powder medium / hard)
+    # keyed by workload; bench.py uses it only for a run of the same units and world size
+    data[f'{a.kernel}@{a.workload}'] = rec
     with open(tpath, 'w') as f:
         json.dump(data, f, indent=1, sort_keys=True)
     print(json.dumps({a.kernel: rec}))

@@ -216,3 +216,64 @@ def test_teleport_maze_matches_oracle(gpu):
     tele = (np.abs(st['qpos'][:, None, :] - outs[None]).max(-1) == 0).any(1)
     assert tele.sum() > 200  # teleported at the last step (earlier ones moved on; all are checked above)
     assert np.array_equal(got_q[tele], st['qpos'][tele])
+
+
+def test_headline_n65536_matches_oracle(gpu):
+    """The BASELINE configuration itself: pointmaze-large, N = 65,536, task
+    i%5+1, Philox reset noise (seed 0), TimeLimit 1000, same-step auto-reset,
+    150 single-step launches vs the OpenMP oracle.  Episode clocks start
+    staggered (elapsed = i % 1000) so that ~15 % of the envs hit the TimeLimit
+    and auto-reset with Philox draws inside the window."""
+    n, k, seed = 65536, 150, 0
+    env = ogbench_amd.make('pointmaze-large-v0', num_envs=n, device=gpu, auto_reset=True)
+    tid = (np.arange(n) % 5 + 1).astype(np.int32)
+    obs, info = env.reset(seed=seed, options=dict(task_id=torch.tensor(tid, device=gpu)))
+    st = orc.reset('large', tid, orc.reset_draws(n, seed))
+    assert np.array_equal(obs.cpu().numpy(), st['qpos']) and np.array_equal(info['goal'].cpu().numpy(), st['goal'])
+    sd = env.state_dict()
+    sd['elapsed'] = torch.tensor(np.arange(n) % 1000, dtype=torch.int32)
+    env.load_state_dict(sd)
+    st['elapsed'][:] = np.arange(n) % 1000
+    acts = (torch.rand(k, n, 2, generator=torch.Generator().manual_seed(1)) * 2 - 1).float()
+    key = orc.philox_key(seed, orc.TAG_MAZE_RESET)
+    resets = 0
+    for t in range(k):
+        o, r, te, tr, inf = env.step(acts[t].to(gpu))
+        ref = orc.step('large', st, acts[t].numpy()[None], auto_reset=1, key=key, nthreads=16)
+        assert np.abs(o.cpu().numpy() - ref['obs'][0]).max() <= TOL, t
+        assert np.array_equal(inf['success'].cpu().numpy(), ref['success'][0].astype(bool)), t
+        assert np.array_equal(te.cpu().numpy(), ref['terminated'][0].astype(bool)), t
+        assert np.array_equal(tr.cpu().numpy(), ref['truncated'][0].astype(bool)), t
+        assert np.array_equal(r.cpu().numpy(), ref['reward'][0]), t
+        resets += int(ref['truncated'][0].sum() + ref['terminated'][0].sum())
+    assert resets >= 0.14 * n
+    assert np.abs(env.get_xy().cpu().numpy() - st['qpos']).max() <= TOL
+    assert np.array_equal(env.cur_goal_xy.cpu().numpy(), st['goal'])
+
+
+@pytest.mark.parametrize('task', [1, 4])
+def test_medium_single_env_timelimit_episode(gpu, task):
+    """pointmaze-medium-v0 with ONE env (BASELINE configs[0], the Gymnasium
+    surface): make -> reset(seed, task_id) -> 1000 steps of U[-1,1]^2 float32
+    actions (torch.Generator seed 0) -> truncated exactly at step 1000, every
+    step against the oracle."""
+    seed = 5 + task
+    env = ogbench_amd.make('pointmaze-medium-v0', num_envs=1, device=gpu)
+    assert env.max_episode_steps == 1000 and env.observation_space.shape == (1, 2)
+    obs, info = env.reset(seed=seed, options=dict(task_id=task))
+    st = orc.reset('medium', np.array([task], np.int32), orc.reset_draws(1, seed))
+    assert np.array_equal(obs.cpu().numpy(), st['qpos']) and np.array_equal(info['goal'].cpu().numpy(), st['goal'])
+    acts = (torch.rand(1000, 1, 2, generator=torch.Generator().manual_seed(0)) * 2 - 1).float()
+    contacts = 0
+    for t in range(1000):
+        prev = env.get_xy().cpu().numpy()
+        o, r, te, tr, inf = env.step(acts[t].to(gpu))
+        ref = orc.step('medium', st, acts[t].numpy()[None])
+        got = o.cpu().numpy()
+        assert np.abs(got - ref['obs'][0]).max() <= TOL, t
+        free = prev + (0.2 * acts[t].numpy()).astype(np.float64)
+        contacts += int(not np.array_equal(got, free))
+        assert bool(te[0]) == bool(ref['terminated'][0, 0]) and bool(inf['success'][0]) == bool(ref['success'][0, 0])
+        assert bool(tr[0]) == (t == 999) == bool(ref['truncated'][0, 0]), t
+        assert float(r[0]) == float(ref['reward'][0, 0])
+    assert contacts > 20  # the episode really exercises wall contacts
