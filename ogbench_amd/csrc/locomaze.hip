@@ -25,6 +25,15 @@
 
 #include "common.h"
 #include "point_physics.h"
+#include "point_contact.h"
+
+// Contact step: the active-set form (point_contact.h) by default;
+// -DOGBX_PHYS_V1 selects the evaluate-and-step form of point_physics.h (A/B only).
+#ifdef OGBX_PHYS_V1
+#define OGBX_POINT_STEP point_step
+#else
+#define OGBX_POINT_STEP point_step_as
+#endif
 
 namespace ogbx {
 
@@ -213,16 +222,23 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
   const MazeParams& P = *Pp;
   OGBX_POINT_MODEL(pm, P);
   __shared__ uint16_t nb_s[kMaxCells];
-  stage_nbmask(P, nb_s);
   const int64_t i = env_of_lane(epw);
-  if (i < 0 || i >= n) return;
+  const bool live = i >= 0 && i < n;
+  // the env's state loads are issued before the wall-mask staging barrier so
+  // that their HBM round trip overlaps it
+  double2 q = make_double2(0.0, 0.0), g = q;
+  int32_t el = 0, task = 1;
+  uint32_t ep = 0;
+  if (live) {
+    q = reinterpret_cast<const double2*>(S.qpos)[i];
+    g = reinterpret_cast<const double2*>(S.goal)[i];
+    el = S.elapsed[i];
+    task = S.task[i];
+    ep = S.episode[i];
+  }
+  stage_nbmask(P, nb_s);
+  if (!live) return;
   const uint64_t gi = (uint64_t)(i + P.env_base);
-
-  double2 q = reinterpret_cast<const double2*>(S.qpos)[i];
-  double2 g = reinterpret_cast<const double2*>(S.goal)[i];
-  int32_t el = S.elapsed[i];
-  int32_t task = S.task[i];
-  uint32_t ep = S.episode[i];
   double x = q.x, y = q.y, gx = g.x, gy = g.y;
   bool reset_any = false;  // goal / episode change only on an auto-reset
 
@@ -242,7 +258,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     if (P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
     x = x + dx;
     y = y + dy;
-    point_step(pm, nb_s, P.H, P.W, &x, &y);
+    OGBX_POINT_STEP(pm, nb_s, P.H, P.W, &x, &y);
     if (!P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
     const double ox = x, oy = y;  // ob is taken before a teleport (maze.py:437-451)
     if (P.n_tp_in > 0) {
@@ -310,7 +326,7 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
     x = x + (double)(0.2f * a[2 * i]);
     y = y + (double)(0.2f * a[2 * i + 1]);
   }
-  int c = point_step(pm, nb_s, P.H, P.W, &x, &y);
+  int c = OGBX_POINT_STEP(pm, nb_s, P.H, P.W, &x, &y);
   qpos_out[2 * i] = x;
   qpos_out[2 * i + 1] = y;
   if (contact_out) contact_out[i] = (uint8_t)c;

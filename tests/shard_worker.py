@@ -9,7 +9,7 @@ its per-env outputs to ``<out>/rank<r>.npz``.  Imported, ``run_maze`` /
 ``run_powder`` give the single-process (G = 1) run the test compares against.
 
 Workloads:
-  pointmaze-large, auto-reset, max_episode_steps 100, task_id = i%5+1 (global
+  pointmaze-large, auto-reset, max_episode_steps 250 (short tasks reach the goal), task_id = i%5+1 (global
   i), Philox reset noise under one shared seed, expert actions (on-device
   oracle-subgoal policy + Philox noise keyed by the global env index);
   powderworld-easy 32x32, auto-reset, random actions with invalid values (the
@@ -35,7 +35,7 @@ def run_maze(base, n, dev, total=MAZE_TOTAL, steps=MAZE_STEPS, seed=SEED):
     import ogbench_amd
     from ogbench_amd.evaluation import accumulate, env_task_ids
 
-    env = ogbench_amd.make('pointmaze-large-v0', num_envs=n, device=dev, auto_reset=True, max_episode_steps=100,
+    env = ogbench_amd.make('pointmaze-large-v0', num_envs=n, device=dev, auto_reset=True, max_episode_steps=250,
                            env_base=base)
     task = (torch.arange(base, base + n, dtype=torch.int32) % 5 + 1).to(dev)
     obs0, info = env.reset(seed=seed, options=dict(task_id=task))
@@ -45,7 +45,7 @@ def run_maze(base, n, dev, total=MAZE_TOTAL, steps=MAZE_STEPS, seed=SEED):
     remaining = torch.full((n,), 1 << 30, dtype=torch.int32, device=dev)
     tid = env_task_ids(env)
     for t in range(steps):
-        a = env.expert_action(noise=0.5, seed=seed)
+        a = env.expert_action(noise=0.2, seed=seed)
         o, r, te, tr, inf = env.step(a)
         accumulate(counters, inf['success'].view(torch.uint8), te.view(torch.uint8), tr.view(torch.uint8), tid,
                    remaining)

@@ -7,7 +7,7 @@ rank * N/2 and one shared seed.  This process runs the same job as ONE batch
 of N envs.  Every per-env output (reset obs/goal, obs, reward, terminated,
 truncated, success, final qpos) must be identical, and the all-gathered eval
 counters must equal the single-run counters.  pointmaze-large: 4096 envs x
-300 steps, expert actions with Philox noise, TimeLimit 100 with auto-reset;
+300 steps, expert actions with Philox noise, TimeLimit 250 with auto-reset;
 powderworld-easy: 128 envs x 30 steps with invalid actions (Philox
 replacements) and auto-reset.
 """
