@@ -100,6 +100,21 @@ __device__ inline void stage_nbmask(const MazeParams& P, uint16_t* nb_s) {
   __syncthreads();
 }
 
+// The step/physics kernels run 256-thread blocks, one thread per entry of the
+// kMaxCells-entry wall-mask table: each thread loads its entry straight from
+// the table's address (no dependent read of H*W), issued together with the
+// env's state and action loads so that the whole prologue is one HBM round
+// trip; nbmask_commit stores it into LDS after them.
+constexpr int kStepBlock = 256;
+static_assert(kMaxCells == kStepBlock, "one wall-mask entry per thread of a step block");
+
+__device__ __forceinline__ uint16_t nbmask_fetch(const MazeParams* Pp) { return Pp->nbmask[threadIdx.x]; }
+
+__device__ __forceinline__ void nbmask_commit(uint16_t* nb_s, uint16_t v) {
+  nb_s[threadIdx.x] = v;
+  __syncthreads();
+}
+
 // np.linalg.norm(xy - goal) <= tol with the 1-D OpenBLAS ddot rounding:
 // sqrt(fma(dy, dy, dx*dx)) (maze.py:487).
 __device__ inline bool goal_reached(double x, double y, double gx, double gy, double tol) {
@@ -224,19 +239,23 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
   __shared__ uint16_t nb_s[kMaxCells];
   const int64_t i = env_of_lane(epw);
   const bool live = i >= 0 && i < n;
-  // the env's state loads are issued before the wall-mask staging barrier so
-  // that their HBM round trip overlaps it
-  double2 q = make_double2(0.0, 0.0), g = q;
+  // one HBM round trip before the first barrier: the wall-mask entry, the
+  // env's state and its first action
+  const uint16_t nbv = nbmask_fetch(Pp);
+  double2 q = make_double2(0.0, 0.0), g = q, a0d = q;
+  float2 a0f = make_float2(0.0f, 0.0f);
   int32_t el = 0, task = 1;
   uint32_t ep = 0;
   if (live) {
+    if (kF64) a0d = reinterpret_cast<const double2*>(action_v)[i];
+    else a0f = reinterpret_cast<const float2*>(action_v)[i];
     q = reinterpret_cast<const double2*>(S.qpos)[i];
     g = reinterpret_cast<const double2*>(S.goal)[i];
     el = S.elapsed[i];
-    task = S.task[i];
     ep = S.episode[i];
+    task = S.task[i];
   }
-  stage_nbmask(P, nb_s);
+  nbmask_commit(nb_s, nbv);
   if (!live) return;
   const uint64_t gi = (uint64_t)(i + P.env_base);
   double x = q.x, y = q.y, gx = g.x, gy = g.y;
@@ -246,11 +265,11 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     const int64_t o = (int64_t)k * n + i;
     double dx, dy;
     if (kF64) {
-      double2 a = reinterpret_cast<const double2*>(action_v)[o];
+      const double2 a = k == 0 ? a0d : reinterpret_cast<const double2*>(action_v)[o];
       dx = 0.2 * a.x;
       dy = 0.2 * a.y;
     } else {
-      float2 a = reinterpret_cast<const float2*>(action_v)[o];
+      const float2 a = k == 0 ? a0f : reinterpret_cast<const float2*>(action_v)[o];
       dx = (double)(0.2f * a.x);  // float32 * weak python float stays float32 (NEP 50)
       dy = (double)(0.2f * a.y);
     }
@@ -310,22 +329,30 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
                                                             const void* action_v, int64_t n,
                                                             double* qpos_out,
                                                             uint8_t* contact_out, int epw) {
-  const MazeParams& P = *Pp;
-  OGBX_POINT_MODEL(pm, P);
+  OGBX_POINT_MODEL(pm, (*Pp));
   __shared__ uint16_t nb_s[kMaxCells];
-  stage_nbmask(P, nb_s);
   const int64_t i = env_of_lane(epw);
-  if (i < 0 || i >= n) return;
-  double x = qpos_in[2 * i], y = qpos_in[2 * i + 1];
-  if (kF64) {
-    const double* a = (const double*)action_v;
-    x = x + 0.2 * a[2 * i];
-    y = y + 0.2 * a[2 * i + 1];
-  } else {
-    const float* a = (const float*)action_v;
-    x = x + (double)(0.2f * a[2 * i]);
-    y = y + (double)(0.2f * a[2 * i + 1]);
+  const bool live = i >= 0 && i < n;
+  const uint16_t nbv = nbmask_fetch(Pp);
+  double x = 0.0, y = 0.0, ax = 0.0, ay = 0.0;
+  if (live) {
+    x = qpos_in[2 * i];
+    y = qpos_in[2 * i + 1];
+    if (kF64) {
+      const double* a = (const double*)action_v;
+      ax = 0.2 * a[2 * i];
+      ay = 0.2 * a[2 * i + 1];
+    } else {
+      const float* a = (const float*)action_v;
+      ax = (double)(0.2f * a[2 * i]);
+      ay = (double)(0.2f * a[2 * i + 1]);
+    }
   }
+  nbmask_commit(nb_s, nbv);
+  if (!live) return;
+  const MazeParams& P = *Pp;
+  x = x + ax;
+  y = y + ay;
   int c = OGBX_POINT_STEP(pm, nb_s, P.H, P.W, &x, &y);
   qpos_out[2 * i] = x;
   qpos_out[2 * i + 1] = y;
@@ -795,7 +822,7 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
   uint32_t k0, k1;
   seed_key(e->seed, kTagMazeReset, &k0, &k1);
   const int epw = e->epw;
-  dim3 grid(grid_for(e->n * (64 / epw), 256)), block(256);
+  dim3 grid(grid_for(e->n * (64 / epw), kStepBlock)), block(kStepBlock);
   if (action_is_f64)
     hipLaunchKernelGGL(maze_step_kernel<true>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
@@ -828,7 +855,7 @@ ogbx_status ogbx_point_physics(ogbx_maze_t e, const double* qpos_in, const void*
   if (n <= 0) return OGBX_OK;
   OGBX_HIP(hipSetDevice(e->device));
   const int epw = e->epw;
-  dim3 grid(grid_for(n * (64 / epw), 256)), block(256);
+  dim3 grid(grid_for(n * (64 / epw), kStepBlock)), block(kStepBlock);
   if (action_is_f64)
     hipLaunchKernelGGL(point_physics_kernel<true>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd,
                        qpos_in, action, n, qpos_out, contact_out, epw);
