@@ -1,8 +1,9 @@
 // point_contact.h -- the pointmaze contact step, active-set form (default).
 //
 // Same model and the same RK4 stage loop as point_physics.h (whose header
-// states every assumed MuJoCo default; wall-contact parity is UNPINNED against
-// MuJoCo itself), with a much shorter per-stage instruction stream.  The step
+// states every assumed MuJoCo default; wall-contact parity is pinned to
+// MuJoCo's published formulation by tests/mjmodel_np.py, not to MuJoCo's
+// output), with a much shorter per-stage instruction stream.  The step
 // kernel runs one wave per SIMD and every wave that holds a contact lane runs
 // the whole 20-stage chain, so the launch time is the instruction count (and
 // dependency depth) of one stage x 20:

@@ -4,7 +4,8 @@
 // the box walls that MazeEnv.update_tree adds (ogbench/locomaze/maze.py:225-239).
 //
 // Model (see DESIGN.md "Point-mass contact model" for every assumed MuJoCo
-// default; wall-contact parity is UNPINNED -- MuJoCo is absent here):
+// default; wall-contact parity is pinned to MuJoCo's published
+// formulation by tests/mjmodel_np.py, not to MuJoCo's output -- MuJoCo is absent):
 //   * M = m*I2, m = density*4/3*pi*r^3 (point.xml:8,28), qacc_smooth = 0
 //     (ctrl never written, gravity orthogonal to both slide axes).
 //   * Contacts: sphere-floor (always active at dist = 0, J_normal = 0 in the

@@ -1,7 +1,9 @@
 """ctypes wrapper of oracle/_build/liboracle.so (oracle/locomaze_ref.c).
 
 TEST INFRASTRUCTURE ONLY -- the checker for libogbx's locomaze kernels.
-Wall-contact dynamics are PARITY UNPINNED (MuJoCo absent); see locomaze_ref.c.
+Wall-contact dynamics are pinned to MuJoCo's published formulation by the
+independent model tests/mjmodel_np.py, not to MuJoCo's output (MuJoCo absent);
+see locomaze_ref.c and DESIGN.md section 6.
 """
 
 import ctypes

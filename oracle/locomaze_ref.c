@@ -9,8 +9,10 @@
  *     success mask, reward/termination/truncation: PINNED by the reference code
  *     (known-answer tests derived from maze.py / point.py, golden tables in
  *     tests/golden/ extracted from the reference source).
- *   - wall-contact dynamics (inside mujoco.mj_step, point.py:73): PARITY
- *     UNPINNED.  MuJoCo (pyproject.toml:12, mujoco >= 3.1.6, no lockfile) is not
+ *   - wall-contact dynamics (inside mujoco.mj_step, point.py:73): pinned to
+ *     MuJoCo's PUBLISHED FORMULATION by tests/mjmodel_np.py (independent
+ *     enumeration model + closed forms, agreement 2e-16), NOT to MuJoCo's
+ *     output: MuJoCo (pyproject.toml:12, mujoco >= 3.1.6, no lockfile) is not
  *     installed and no reference trajectories exist; this file restates the
  *     published MuJoCo soft-constraint algorithm with the defaults listed in
  *     DESIGN.md.  It is written independently of the HIP kernel: literal
