@@ -145,6 +145,21 @@ ogbx_status ogbx_maze_step(ogbx_maze_t env, const void* action, int32_t action_i
                            uint8_t* truncated, uint8_t* success, double* final_obs,
                            int32_t auto_reset, void* stream);
 
+/* Evaluation rollout without auto-reset: env i steps with actions device
+ * [k_steps, N, 2] until the first step that ends its episode (terminated |
+ * truncated) or k_steps, in ONE launch; rows k >= steps_taken[i] of the
+ * outputs (same layout as ogbx_maze_step) are left untouched, and the env's
+ * state is the state after its last step.  Replaces the reference's
+ * evaluation episode loop `while not done: env.step(...)`
+ * (impls/utils/evaluation.py:83-112) for a batch of episodes; a wave of 64
+ * envs leaves the loop when a ballot finds all of them done.
+ * Every written row equals what K calls of ogbx_maze_step (auto_reset 0)
+ * produce. */
+ogbx_status ogbx_maze_rollout_until_done(ogbx_maze_t env, const void* action, int32_t action_is_f64,
+                                         int32_t k_steps, double* obs, float* reward, uint8_t* terminated,
+                                         uint8_t* truncated, uint8_t* success, int32_t* steps_taken,
+                                         void* stream);
+
 /* Device pointers of the env-owned state (for checkpoint/restore and tests):
  * qpos f64[N,2], goal_xy f64[N,2], elapsed i32[N], task_id i32[N],
  * episode u32[N] (per-env reset counter = the Philox counter word of that

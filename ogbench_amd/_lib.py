@@ -78,6 +78,10 @@ _SIGNATURES = {
         [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_int32, c_void_p],
     ),
+    'ogbx_maze_rollout_until_done': (
+        c_int32,
+        [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     'ogbx_maze_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p)]),
     'ogbx_point_physics': (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p, c_void_p]),
     'ogbx_maze_xy_to_ij': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),

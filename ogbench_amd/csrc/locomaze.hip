@@ -227,13 +227,19 @@ __global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __res
 
 // One launch = k_steps consecutive env steps of every env; state stays in
 // registers across the k loop.  One lane per env.
-template <bool kF64>
+// kUntilDone (no auto-reset): an env stops at the first step that ends its
+// episode (terminated | truncated); its later rows are not written and
+// steps_taken[i] counts the rows it wrote.  A wave leaves the k loop as soon as
+// a ballot finds every lane done, so a batch of evaluation episodes costs the
+// steps of its longest episode per wave, not k_steps.
+template <bool kF64, bool kUntilDone>
 __global__ void __launch_bounds__(256) maze_step_kernel(
     const MazeParams* __restrict__ Pp, MazeState S, int64_t n, const void* __restrict__ action_v,
     int32_t k_steps,
     double* __restrict__ obs, float* __restrict__ reward, uint8_t* __restrict__ terminated,
     uint8_t* __restrict__ truncated, uint8_t* __restrict__ success,
-    double* __restrict__ final_obs, int32_t auto_reset, uint32_t k0, uint32_t k1, int epw) {
+    double* __restrict__ final_obs, int32_t auto_reset, uint32_t k0, uint32_t k1, int epw,
+    int32_t* __restrict__ steps_taken) {
   const MazeParams& P = *Pp;
   OGBX_POINT_MODEL(pm, P);
   __shared__ uint16_t nb_s[kMaxCells];
@@ -260,8 +266,14 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
   const uint64_t gi = (uint64_t)(i + P.env_base);
   double x = q.x, y = q.y, gx = g.x, gy = g.y;
   bool reset_any = false;  // goal / episode change only on an auto-reset
+  bool done = false;       // kUntilDone: this env's episode has ended
+  int32_t taken = 0;
 
   for (int32_t k = 0; k < k_steps; ++k) {
+    if (kUntilDone) {
+      if (__all(done)) break;  // wave-uniform early exit (ballot over live lanes)
+      if (done) continue;
+    }
     const int64_t o = (int64_t)k * n + i;
     double dx, dy;
     if (kF64) {
@@ -314,9 +326,14 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
       wy = y;
     }
     reinterpret_cast<double2*>(obs)[o] = make_double2(wx, wy);
+    if (kUntilDone) {
+      taken = k + 1;
+      done = term || trunc;
+    }
   }
   reinterpret_cast<double2*>(S.qpos)[i] = make_double2(x, y);
   S.elapsed[i] = el;
+  if (kUntilDone) steps_taken[i] = taken;
   if (reset_any) {
     reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
     S.episode[i] = ep;
@@ -626,8 +643,10 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
   e->device = device;
   if (const char* v = std::getenv("OGBX_MAZE_LDS")) {  // diagnostic placement knob (A/B only)
     e->lds_pad = std::atoi(v);
-    hipFuncSetAttribute((const void*)maze_step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
-    hipFuncSetAttribute((const void*)maze_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    hipFuncSetAttribute((const void*)maze_step_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    hipFuncSetAttribute((const void*)maze_step_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    hipFuncSetAttribute((const void*)maze_step_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    hipFuncSetAttribute((const void*)maze_step_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
     hipFuncSetAttribute((const void*)point_physics_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
     hipFuncSetAttribute((const void*)point_physics_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
   }
@@ -824,13 +843,39 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
   const int epw = e->epw;
   dim3 grid(grid_for(e->n * (64 / epw), kStepBlock)), block(kStepBlock);
   if (action_is_f64)
-    hipLaunchKernelGGL(maze_step_kernel<true>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
+    hipLaunchKernelGGL((maze_step_kernel<true, false>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
-                       final_obs, auto_reset, k0, k1, epw);
+                       final_obs, auto_reset, k0, k1, epw, nullptr);
   else
-    hipLaunchKernelGGL(maze_step_kernel<false>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
+    hipLaunchKernelGGL((maze_step_kernel<false, false>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
-                       final_obs, auto_reset, k0, k1, epw);
+                       final_obs, auto_reset, k0, k1, epw, nullptr);
+  OGBX_LAUNCHED("maze_step_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_rollout_until_done(ogbx_maze_t e, const void* action, int32_t action_is_f64,
+                                         int32_t k_steps, double* obs, float* reward, uint8_t* terminated,
+                                         uint8_t* truncated, uint8_t* success, int32_t* steps_taken,
+                                         void* stream) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
+  OGBX_CHECK(e->P.loco_type == 0, OGBX_EINVAL,
+             "only the point-mass dynamics are implemented (ant/humanoid are wrapper-only)");
+  OGBX_CHECK(action && obs && reward && terminated && truncated && success && steps_taken, OGBX_EINVAL,
+             "ogbx_maze_rollout_until_done: null argument");
+  OGBX_CHECK(k_steps >= 1, OGBX_EINVAL, "k_steps must be >= 1");
+  OGBX_HIP(hipSetDevice(e->device));
+  const int epw = e->epw;
+  dim3 grid(grid_for(e->n * (64 / epw), kStepBlock)), block(kStepBlock);
+  if (action_is_f64)
+    hipLaunchKernelGGL((maze_step_kernel<true, true>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
+                       e->n, action, k_steps, obs, reward, terminated, truncated, success, nullptr, 0, 0u, 0u,
+                       epw, steps_taken);
+  else
+    hipLaunchKernelGGL((maze_step_kernel<false, true>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
+                       e->n, action, k_steps, obs, reward, terminated, truncated, success, nullptr, 0, 0u, 0u,
+                       epw, steps_taken);
   OGBX_LAUNCHED("maze_step_kernel");
   return OGBX_OK;
 }

@@ -470,6 +470,50 @@ class MazeEnv:
         )
         return out
 
+    def rollout_until_done(self, actions, out=None):
+        """Evaluation episodes in ONE launch (no auto-reset): env i steps with
+        actions[k, i] until its episode ends (terminated | truncated) or the K
+        actions run out -- the reference's ``while not done: env.step(...)``
+        loop (impls/utils/evaluation.py:83-112) for the whole batch.
+
+        Returns the rollout dict of ``rollout`` plus ``steps`` (int32 [N], rows
+        written per env); rows k >= steps[i] are left as they were.  Each wave
+        of 64 envs stops once all its episodes ended."""
+        torch = _torch()
+        if self.auto_reset:
+            raise ValueError('rollout_until_done needs auto_reset=False (an auto-reset episode never ends)')
+        a = self._action(actions)
+        K = a.shape[0]
+        if a.shape != (K, self.num_envs, 2):
+            raise ValueError(f'actions must have shape (K, {self.num_envs}, 2)')
+        if out is None:
+            kw = dict(device=self.device)
+            out = dict(
+                obs=torch.zeros(K, self.num_envs, 2, dtype=torch.float64, **kw),
+                reward=torch.zeros(K, self.num_envs, dtype=torch.float32, **kw),
+                terminated=torch.zeros(K, self.num_envs, dtype=torch.uint8, **kw),
+                truncated=torch.zeros(K, self.num_envs, dtype=torch.uint8, **kw),
+                success=torch.zeros(K, self.num_envs, dtype=torch.uint8, **kw),
+                steps=torch.zeros(self.num_envs, dtype=torch.int32, **kw),
+            )
+        _lib.check(
+            self._L.ogbx_maze_rollout_until_done(
+                self._h,
+                _lib.ptr(a),
+                int(a.dtype == torch.float64),
+                K,
+                _lib.ptr(out['obs']),
+                _lib.ptr(out['reward']),
+                _lib.ptr(out['terminated']),
+                _lib.ptr(out['truncated']),
+                _lib.ptr(out['success']),
+                _lib.ptr(out['steps']),
+                self._stream(),
+            ),
+            'rollout_until_done',
+        )
+        return out
+
     def physics(self, qpos, action):
         """Free-standing PointEnv physics (point.py:68-73) for [n,2] qpos/actions."""
         torch = _torch()

@@ -154,6 +154,59 @@ def test_env_rollout_matches_oracle(gpu, fused):
     assert ref['truncated'].sum() > 0
 
 
+@pytest.mark.parametrize('f64', [False, True])
+def test_rollout_until_done_matches_single_steps(gpu, f64):
+    """Evaluation rollout (no auto-reset, SURVEY 7.3 wave-ballot exit): every
+    row an env writes equals K single env.step calls; rows after its episode
+    ended are untouched; the env's state is the state at its last step."""
+    n, k = 4096, 200
+    kw = dict(max_episode_steps=150)
+    rng = np.random.RandomState(11)
+    tid = torch.tensor((np.arange(n) % 5 + 1).astype(np.int32))
+    noise = torch.tensor(rng.uniform(-1, 1, (n, 4)))
+    envs = [_env(gpu, n, 'large', **kw) for _ in range(2)]
+    obs0 = [e.reset(seed=5, options=dict(task_id=tid, noise=noise))[0] for e in envs]
+    # goals within a few units of the start (half of the envs), the task goal
+    # otherwise; heading straight for them ends some episodes at the goal and
+    # the rest at the TimeLimit
+    sd = envs[0].state_dict()
+    near = torch.tensor(rng.uniform(-3, 3, (n, 2)), device=gpu) + obs0[0]
+    sd['goal'] = torch.where(torch.arange(n, device=gpu)[:, None] % 2 == 0, near, sd['goal'])
+    for e in envs:
+        e.load_state_dict(sd)
+    goal = sd['goal'].cpu().numpy()
+    d = goal - obs0[0].cpu().numpy()
+    acts = np.clip(d / np.maximum(np.abs(d).max(1, keepdims=True), 1e-9), -1, 1)
+    acts = np.repeat(acts[None], k, 0) + rng.normal(0, 0.3, (k, n, 2))
+    acts = torch.tensor(np.clip(acts, -1, 1).astype(np.float64 if f64 else np.float32))
+    sentinel = -7.0
+    out = dict(obs=torch.full((k, n, 2), sentinel, dtype=torch.float64, device=gpu),
+               reward=torch.full((k, n), sentinel, dtype=torch.float32, device=gpu),
+               terminated=torch.full((k, n), 9, dtype=torch.uint8, device=gpu),
+               truncated=torch.full((k, n), 9, dtype=torch.uint8, device=gpu),
+               success=torch.full((k, n), 9, dtype=torch.uint8, device=gpu),
+               steps=torch.zeros(n, dtype=torch.int32, device=gpu))
+    got = {key: v.cpu().numpy() for key, v in envs[0].rollout_until_done(acts, out).items()}
+    steps = got['steps']
+    ref = dict(obs=[], reward=[], terminated=[], truncated=[], success=[])
+    for t in range(k):
+        o, r, te, tr, info = envs[1].step(acts[t])
+        for key, v in (('obs', o), ('reward', r), ('terminated', te), ('truncated', tr), ('success', info['success'])):
+            ref[key].append(v.cpu().numpy().copy())
+    ref = {key: np.stack(v) for key, v in ref.items()}
+    done = ref['terminated'].astype(bool) | ref['truncated'].astype(bool)
+    first = np.where(done.any(0), done.argmax(0) + 1, k)
+    assert np.array_equal(steps, first)
+    assert (first < 150).sum() > 100 and (first == 150).sum() > 100  # goal ends and TimeLimit ends
+    rows = np.arange(k)[:, None] < steps[None, :]
+    for key in ('obs', 'reward', 'terminated', 'truncated', 'success'):
+        g, r = got[key], ref[key].astype(got[key].dtype)
+        assert np.array_equal(g[rows], r[rows]), key
+        assert (g[~rows] == (sentinel if key in ('obs', 'reward') else 9)).all(), key
+    final = got['obs'][steps - 1, np.arange(n)]
+    assert np.array_equal(envs[0].get_xy().cpu().numpy(), final)
+
+
 def test_truncation_singletask_reward(gpu):
     n = 64
     env = ogbench_amd.make('pointmaze-medium-singletask-task2-v0', num_envs=n, device=gpu, max_episode_steps=4)
