@@ -778,6 +778,104 @@ def cpu_baseline_powder_full(ne, size, args):
                        f'({dt:.1f} s; goal replays excluded)')
 
 
+ANT_BYTES = 15 * 8 + 14 * 8  # one body state row (qpos 15 + qvel 14, f64)
+
+
+def bench_antmaze(args, world, rank, dev):
+    """antmaze-large-navigate-v0 wrapper (BASELINE configs[4]: N = 131,072 over
+    8 GPUs = 16,384 envs per rank, weak scaling): one step = ogbx_antmaze_step
+    over this rank's envs consuming a caller-supplied post-physics body state
+    (a ring of 8 synthetic snapshots standing in for the out-of-scope ant
+    dynamics), same-step auto-reset with Philox reset bodies, task i%5+1 of
+    the global env index.  Algorithmic bytes per env-step: post-physics row
+    read 232 + body state write 232 + ob write 232 + goal 16 + elapsed 8 +
+    reward/flags 7 = 727 B (SURVEY 8d prices the same contract at 759 B with
+    the physics engine's action read, which the wrapper does not touch)."""
+    import ogbench_amd
+    from ogbench_amd.evaluation import accumulate, env_task_ids, gather_counters, summarize
+
+    n = args.num_envs if args.num_envs != 65536 else 16384
+    base = rank * n
+    env = ogbench_amd.MazeEnv('ant', 'large', num_envs=n, device=dev, auto_reset=True, env_base=base)
+    tid = (torch.arange(base, base + n, dtype=torch.int32, device=dev) % 5) + 1
+    obs0, info = env.reset(seed=0, options=dict(task_id=tid))
+    R = 8
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + rank)
+    goal = info['goal'].clone()
+    start = obs0[:, :2].clone()
+    ring_q = torch.randn(R, n, 15, device=dev, dtype=torch.float64, generator=gen)
+    ring_v = torch.randn(R, n, 14, device=dev, dtype=torch.float64, generator=gen)
+    # snapshots walk part of the way to the goal: some envs reach it (success,
+    # termination, auto-reset), the rest run to the TimeLimit
+    frac = (torch.rand(n, 1, device=dev, dtype=torch.float64, generator=gen) * 1.25).clamp(max=1.0)
+    for k in range(R):
+        ring_q[k, :, :2] = start + (goal - start) * frac * (k + 1) / R
+
+    def step(i):
+        env.wrap_step(ring_q[i % R], ring_v[i % R])
+
+    for i in range(args.warmup):
+        step(i)
+    dt = _timed(step, args.steps, world, dev)
+    value = n * world * args.steps / dt
+    kern_ms, kern_info = _launch_ms(step, max(1000, min(args.steps, 2000)), dev)
+    per = 3 * ANT_BYTES + 16 + 8 + 7
+    achieved = per * n / (kern_ms * 1e-3) / 1e9
+    extra = {}
+    if not args.no_extras:
+        # untimed eval reduction over the wrapper's flags (SURVEY 8e)
+        counters = torch.zeros(env.num_tasks, 2, dtype=torch.int64, device=dev)
+        remaining = torch.ones(n, dtype=torch.int32, device=dev)
+        ids = env_task_ids(env)
+        for i in range(1000):
+            _, _, te, tr, inf = env.wrap_step(ring_q[i % R], ring_v[i % R])
+            accumulate(counters, inf['success'].view(torch.uint8), te.view(torch.uint8), tr.view(torch.uint8), ids,
+                       remaining)
+        total, per_rank = gather_counters(counters)
+        m = summarize(total, env.task_infos)
+        extra['eval_allgather'] = dict(episodes=int(total[:, 1].sum()), ranks=int(per_rank.shape[0]),
+                                       policy='synthetic post-physics ring',
+                                       overall_success=m.get('evaluation/overall_success'))
+    result = dict(
+        metric='antmaze wrapper env steps/sec, antmaze-large-navigate-v0, 16384 envs per GPU',
+        value=value, unit='env_steps/s', n_gpus=world, steps=args.steps, warmup=args.warmup,
+        ms_per_step=dt / args.steps * 1e3, higher_is_better=True, scaling='weak', vs_baseline=None, dtype='f64',
+        data='synthetic post-physics ant states (ring of 8 snapshots; ant dynamics out of scope), Philox resets',
+        config=dict(workload='antmaze-large-navigate-v0 wrapper', num_envs_per_gpu=n, total_envs=n * world,
+                    auto_reset=True, task_id='i%5+1', parallelism=f'env-shard x{world} (global env_base)'),
+        roofline=dict(bound='hbm', kernel='ant_step_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('ant_step_kernel', 'antmaze', n, world),
+                      kernel_ms=kern_ms, **kern_info, alg_bytes_per_launch=per * n),
+        extra=extra,
+    )
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result['cpu_baseline'] = cpu_baseline_antmaze(n, args)
+    env.close()
+    return result
+
+
+def cpu_baseline_antmaze(n, args):
+    """oracle/antmaze_np.py (NumPy, 1 core) on the same workload shape."""
+    from oracle import antmaze_np as am
+
+    rng = np.random.RandomState(0)
+    task = np.arange(n) % 5 + 1
+    b = am.Batch(task, rng.uniform(-1, 1, (n, 4)), np.concatenate(
+        [rng.uniform(-0.1, 0.1, (n, 15)), rng.standard_normal((n, 14))], 1))
+    R = 8
+    qs = [rng.standard_normal((n, 15)) for _ in range(R)]
+    vs = [rng.standard_normal((n, 14)) for _ in range(R)]
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < min(args.cpu_seconds, 10.0):
+        b.step(qs[steps % R], vs[steps % R], auto_reset=True, rng=rng)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n * steps / dt, unit='env_steps/s', cores=1, kind='port',
+                sample=f'{steps} steps x {n} envs of the wrapper with auto-reset ({dt:.1f} s)')
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -785,7 +883,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=100)
     ap.add_argument('--workload', default='pointmaze',
                     choices=['pointmaze', 'pointmaze-medium-n1', 'powder', 'powder-medium', 'powder-hard', 'gcsample',
-                             'hgcsample'])
+                             'hgcsample', 'antmaze'])
     ap.add_argument('--num-envs', type=int, default=65536)
     ap.add_argument('--ring', type=int, default=128)
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
@@ -801,7 +899,8 @@ def main():
     import sys
 
     sys.path.insert(0, ROOT)
-    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, **{'pointmaze-medium-n1': bench_pointmaze_n1}, gcsample=bench_gcsample, hgcsample=bench_hgcsample,
+    fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, **{'pointmaze-medium-n1': bench_pointmaze_n1},
+              gcsample=bench_gcsample, hgcsample=bench_hgcsample, antmaze=bench_antmaze,
               **{'powder-medium': lambda *a: bench_powder(*a, level='medium'),
                  'powder-hard': lambda *a: bench_powder(*a, level='hard')})[args.workload]
     result = fn(args, world, rank, dev)

@@ -145,6 +145,50 @@ ogbx_status ogbx_maze_step(ogbx_maze_t env, const void* action, int32_t action_i
                            uint8_t* truncated, uint8_t* success, double* final_obs,
                            int32_t auto_reset, void* stream);
 
+/* ---- antmaze wrapper (loco_type 1): the maze layer around caller-supplied
+ * ant physics.  The ant's articulated dynamics (AntEnv.do_simulation ->
+ * mujoco.mj_step x5, ogbench/locomaze/ant.py:69-95) are out of scope: the
+ * caller's physics engine advances the body state; these entry points do what
+ * MazeEnv.reset / MazeEnv.step + TimeLimit do around it (maze.py:373-466) at
+ * the AntEnv layout (qpos f64[15], qvel f64[14], ob = concat(qpos, qvel) f64[29],
+ * xy = qpos[:2], goal_tol 0.5; ant.py:97-122, maze.py:86).  Wrapper parity is
+ * pinned by the reference's own methods (tests/golden/antmaze_golden.npz);
+ * ant dynamics are unpinned and not implemented. */
+
+/* The handle's body state: device f64[N,15] qpos and f64[N,14] qvel, the
+ * buffers an in-place physics engine reads and overwrites each step. */
+ogbx_status ogbx_antmaze_state(ogbx_maze_t env, double** body_qpos, double** body_qvel);
+
+/* MazeEnv.reset for an ant handle (maze.py:373-431): task / init_xy / goal_xy
+ * exactly as ogbx_maze_reset (same task_id, task_xy, mask, noise and seed
+ * semantics); body = AntEnv.reset_model (ant.py:103-111): qpos = qpos0 +
+ * uniform(-0.1, 0.1)^15, qvel = 0.1 * normal^14, then set_xy(init_xy).
+ *   body_draws  device f64[N,29] = the 15 uniform(-0.1,0.1) and 14 standard
+ *               normal draws in reset_model order, or NULL = Philox.
+ *   obs         device f64[N,29] out; goal device f64[N,2] out (the goal xy:
+ *               info['goal'] as the oracle representation -- the full goal
+ *               observation needs physics, maze.py:407-418). */
+ogbx_status ogbx_antmaze_reset(ogbx_maze_t env, const int32_t* task_id, const double* task_xy,
+                               const uint8_t* mask, const double* noise, const double* body_draws,
+                               double* obs, double* goal, uint64_t seed, void* stream);
+
+/* MazeEnv.step + TimeLimit for an ant handle, given the post-physics state
+ * qpos_post f64[N,15] / qvel_post f64[N,14] -- either the handle's own state
+ * (ogbx_antmaze_state, stepped in place by the physics engine) or separate
+ * buffers (copied into the handle's state).  Outputs [N]: obs f64[N,29] (the
+ * post-physics ob, taken before a teleport), reward f32, terminated /
+ * truncated / success u8; success on qpos[:2] (post, or the previous xy for
+ * success_timing 'pre').  Teleport mazes move qpos[:2] as ogbx_maze_step does.
+ * auto_reset != 0: envs that end are reset in the same step (Philox xy draws
+ * with the seed of the last reset, task kept); their body is reset_states
+ * f64[N,29] (the caller's own reset state rows, xy replaced by init_xy) or,
+ * when NULL, the Philox reset_model draws; final_obs (nullable) f64[N,29]
+ * receives their pre-reset ob. */
+ogbx_status ogbx_antmaze_step(ogbx_maze_t env, const double* qpos_post, const double* qvel_post,
+                              double* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+                              uint8_t* success, double* final_obs, int32_t auto_reset,
+                              const double* reset_states, void* stream);
+
 /* Evaluation rollout without auto-reset: env i steps with actions device
  * [k_steps, N, 2] until the first step that ends its episode (terminated |
  * truncated) or k_steps, in ONE launch; rows k >= steps_taken[i] of the

@@ -78,6 +78,16 @@ _SIGNATURES = {
         [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_int32, c_void_p],
     ),
+    'ogbx_antmaze_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p)]),
+    'ogbx_antmaze_reset': (
+        c_int32,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p],
+    ),
+    'ogbx_antmaze_step': (
+        c_int32,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+         c_void_p, c_void_p],
+    ),
     'ogbx_maze_rollout_until_done': (
         c_int32,
         [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

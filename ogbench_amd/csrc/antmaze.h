@@ -1,0 +1,245 @@
+// antmaze.h -- the antmaze wrapper (loco_type 'ant') around caller-supplied
+// ant physics: the maze layer of the reference's MazeEnv (ogbench/locomaze/
+// maze.py:373-466) at the AntEnv state layout (ogbench/locomaze/ant.py:69-122),
+// batched over N envs.  Included by locomaze.hip (MazeParams, MazeState,
+// reset_draws, reset_one, goal_reached).
+//
+// State in HBM per env: body qpos f64[15] (free joint xyz + quat, 8 hinges)
+// and qvel f64[14] (the ant's nq/nv, ant.xml), plus the maze state shared with
+// the point env (goal, elapsed, task, episode, and xy = get_xy() after the last
+// step, which 'pre' success timing reads).  The articulated dynamics
+// (AntEnv.do_simulation -> mj_step x5) are NOT here: the caller's physics
+// engine advances the body state and hands the post-physics state to
+// ogbx_antmaze_step, which does everything MazeEnv.step + TimeLimit do with it:
+//   ob = concat(qpos, qvel)                         (ant.py:97-101, before any teleport)
+//   success = |qpos[:2] - goal| <= 0.5 (fma norm)   (maze.py:86,486-490; pre or post)
+//   teleport: qpos[:2] := a Philox-drawn out-portal (maze.py:442-451)
+//   terminated = success & terminate_at_goal; reward = success (-1 single-task)
+//   truncated = (++elapsed >= max_episode_steps)    (gymnasium TimeLimit)
+//   optional same-step auto-reset (below).
+// Reset (maze.py:373-431 with AntEnv.reset_model, ant.py:103-111): the
+// returned ob is the second reset's state, qpos = init_qpos + U(-0.1, 0.1)^15,
+// qvel = 0.1 N(0,1)^14, then set_xy(init_xy) -- no physics.  (The first reset
+// + 5 random steps only feed info['goal'] as a full observation, which needs
+// the physics engine; the wrapper returns the goal xy, i.e. the oracle rep.)
+// The body draws come from Philox (tag kTagAntBody) or from the caller:
+// injected draws [N,29] (parity) or whole reset states [N,29] produced by the
+// caller's own physics reset (auto-reset), whose xy is then set to init_xy.
+#pragma once
+
+namespace ogbx {
+
+constexpr int kAntNq = 15, kAntNv = 14, kAntOb = kAntNq + kAntNv;
+constexpr uint32_t kTagAntBody = 0x414E0001u;
+
+// ant.xml qpos0: torso at (0, 0, 0.75), unit quaternion, hinges at 0.
+__device__ __forceinline__ double ant_init_qpos(int c) {
+  return c == 2 ? 0.75 : (c == 3 ? 1.0 : 0.0);
+}
+
+// The c-th body draw of env gi's episode ep: c < 15 -> uniform(-0.1, 0.1),
+// c >= 15 -> standard normal (Box-Muller on two Philox uniforms).
+__device__ inline double ant_body_draw(uint64_t gi, uint32_t ep, int c, uint32_t k0, uint32_t k1) {
+  const u32x4 w = philox4x32_10({(uint32_t)gi, ep, 0x300u + (uint32_t)c, (uint32_t)(gi >> 32)}, k0 ^ kTagAntBody, k1);
+  const double u0 = u01_from(w.x, w.y), u1 = u01_from(w.z, w.w);
+  if (c < kAntNq) return -0.1 + 0.2 * u0;
+  const double r = sqrt(-2.0 * log1p(-u0));  // 1 - u0 in (0, 1]
+  return r * cospi(2.0 * u1);
+}
+
+// One env's reset body state into q[15], v[14] with xy := (x, y).
+// draws: injected [29] (uniform(-0.1,0.1) x15, N(0,1) x14) or NULL (Philox);
+// states: a whole caller reset state [29] (qpos, qvel) or NULL.
+__device__ inline void ant_reset_body(uint64_t gi, uint32_t ep, uint32_t k0, uint32_t k1, const double* draws,
+                                      const double* states, double x, double y, double* q, double* v) {
+  for (int c = 0; c < kAntNq; ++c)
+    q[c] = states ? states[c] : ant_init_qpos(c) + (draws ? draws[c] : ant_body_draw(gi, ep, c, k0, k1));
+  for (int c = 0; c < kAntNv; ++c) {
+    const int d = kAntNq + c;
+    v[c] = states ? states[d] : 0.0 + 0.1 * (draws ? draws[d] : ant_body_draw(gi, ep, d, k0, k1));
+  }
+  q[0] = x;  // set_xy(init_xy) (ant.py:118-122)
+  q[1] = y;
+}
+
+// MazeEnv.reset for ant handles.  One lane per env; row writes are strided
+// (reset is off the step path).
+__global__ void __launch_bounds__(256) ant_reset_kernel(const MazeParams* __restrict__ Pp, MazeState S,
+                                                        double* __restrict__ bq, double* __restrict__ bv, int64_t n,
+                                                        const int32_t* task_id, const double* task_xy,
+                                                        const uint8_t* mask, const double* noise,
+                                                        const double* body_draws, double* obs, double* goal_out,
+                                                        uint32_t k0, uint32_t k1) {
+  const MazeParams& P = *Pp;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (mask != nullptr && mask[i] == 0) return;
+  const uint32_t ep = S.episode[i] + 1u;
+  const uint64_t gi = (uint64_t)(i + P.env_base);
+  int32_t task;
+  if (P.reward_task_id > 0) task = P.reward_task_id;
+  else if (task_id != nullptr) task = task_id[i];
+  else task = draw_task(P, gi, ep, k0, k1);
+  if (task < 1 || task > P.num_tasks) task = 1;
+  double r[4];
+  if (noise != nullptr) {
+    for (int k = 0; k < 4; ++k) r[k] = noise[4 * i + k];
+  } else {
+    reset_draws(gi, ep, k0, k1, r);
+  }
+  double x, y, gx, gy;
+  reset_one(P, task, task_xy ? task_xy + 4 * i : nullptr, r, x, y, gx, gy);
+  double q[kAntNq], v[kAntNv];
+  ant_reset_body(gi, ep, k0, k1, body_draws ? body_draws + (int64_t)kAntOb * i : nullptr, nullptr, x, y, q, v);
+  for (int c = 0; c < kAntNq; ++c) {
+    bq[kAntNq * i + c] = q[c];
+    obs[kAntOb * i + c] = q[c];
+  }
+  for (int c = 0; c < kAntNv; ++c) {
+    bv[kAntNv * i + c] = v[c];
+    obs[kAntOb * i + kAntNq + c] = v[c];
+  }
+  S.qpos[2 * i] = x;
+  S.qpos[2 * i + 1] = y;
+  S.goal[2 * i] = gx;
+  S.goal[2 * i + 1] = gy;
+  S.elapsed[i] = 0;
+  S.task[i] = task;
+  S.episode[i] = ep;
+  goal_out[2 * i] = gx;
+  goal_out[2 * i + 1] = gy;
+}
+
+// Row kinds decided in phase A of ant_step_kernel.
+constexpr uint8_t kRowPlain = 0, kRowTeleport = 1, kRowReset = 2;
+// 64 envs per 256-thread block: phase A on the first wave, phase B's
+// 64 x 29 elements spread over all four (8 per thread), so a launch at the
+// 16,384 envs of one 8-GPU share has 1,024 waves with short streams.
+constexpr int kAntEnvs = 64, kAntThreads = 256;
+constexpr int kAntPer = (kAntEnvs * kAntOb + kAntThreads - 1) / kAntThreads;
+
+// One wrapper step of kAntEnvs envs per block.
+//   phase A (one lane per env): success / teleport / TimeLimit / reward and
+//     flags; auto-reset rows are written whole by their lane (rare);
+//   phase B (the block's [64 x 29] obs rows as one flat range): ob = the
+//     post-physics (qpos, qvel) row, coalesced; the body state takes the
+//     post-physics row (copied unless the caller stepped it in place) with the
+//     teleported xy.  Phase B's loads are issued before phase A, so the
+//     block pays one HBM round trip before its stores.
+__global__ void __launch_bounds__(kAntThreads) ant_step_kernel(
+    const MazeParams* __restrict__ Pp, MazeState S, double* __restrict__ bq, double* __restrict__ bv, int64_t n,
+    const double* __restrict__ qpost, const double* __restrict__ vpost, int32_t in_place,
+    double* __restrict__ obs, float* __restrict__ reward, uint8_t* __restrict__ terminated,
+    uint8_t* __restrict__ truncated, uint8_t* __restrict__ success, double* __restrict__ final_obs,
+    int32_t auto_reset, const double* __restrict__ reset_states, uint32_t k0, uint32_t k1) {
+  const MazeParams& P = *Pp;
+  __shared__ uint8_t kind_s[kAntEnvs];
+  __shared__ double2 xy_s[kAntEnvs];
+  const int64_t base = (int64_t)blockIdx.x * kAntEnvs;
+  const int nb = (int)(n - base < (int64_t)kAntEnvs ? n - base : (int64_t)kAntEnvs);
+  const int tot = nb * kAntOb;
+  // block-local rows (32-bit offsets from here on)
+  const double* qb = qpost + kAntNq * base;
+  const double* vb = vpost + kAntNv * base;
+  double val[kAntPer];
+#pragma unroll
+  for (int r = 0; r < kAntPer; ++r) {
+    const int f = (int)threadIdx.x + kAntThreads * r;
+    const int e = f / kAntOb, c = f - e * kAntOb;
+    val[r] = 0.0;
+    if (f < tot) val[r] = c < kAntNq ? qb[kAntNq * e + c] : vb[kAntNv * e + (c - kAntNq)];
+  }
+  const int64_t i = base + threadIdx.x;
+  if (threadIdx.x < kAntEnvs && i < n) {
+    const double2 g = reinterpret_cast<const double2*>(S.goal)[i];
+    const double px = qpost[kAntNq * i], py = qpost[kAntNq * i + 1];
+    int32_t el = S.elapsed[i];
+    // pre timing: the xy the previous step (or reset) left, kept in S.qpos
+    // because an in-place physics engine has already overwritten the body
+    double2 pre = make_double2(px, py);
+    if (P.success_pre) pre = reinterpret_cast<const double2*>(S.qpos)[i];
+    const bool succ = goal_reached(pre.x, pre.y, g.x, g.y, P.goal_tol);
+    uint8_t kind = kRowPlain;
+    double nx = px, ny = py;
+    if (P.n_tp_in > 0) {
+      for (int t = 0; t < P.n_tp_in; ++t) {
+        if (goal_reached(px, py, P.tp_in[t][0], P.tp_in[t][1], P.tp_radius * 1.5)) {
+          const uint64_t gi = (uint64_t)(i + P.env_base);
+          const uint32_t ep = S.episode[i];
+          const u32x4 c = philox4x32_10({(uint32_t)gi, ep, 0x100u + (uint32_t)el, (uint32_t)(gi >> 32)},
+                                        k0 ^ kTagMazeTeleport, k1);
+          const int o = (int)bounded_u32(c.x, (uint32_t)P.n_tp_out);
+          nx = P.tp_out[o][0];
+          ny = P.tp_out[o][1];
+          kind = kRowTeleport;
+          break;
+        }
+      }
+    }
+    float rew = succ ? 1.0f : 0.0f;
+    if (P.reward_task_id > 0) rew -= 1.0f;
+    const bool term = succ && P.terminate_at_goal;
+    el += 1;
+    const bool trunc = el >= P.max_steps;
+    reward[i] = rew;
+    terminated[i] = term;
+    truncated[i] = trunc;
+    success[i] = succ;
+    if (auto_reset && (term || trunc)) {
+      kind = kRowReset;
+      if (final_obs != nullptr) {  // the pre-reset observation
+        for (int c = 0; c < kAntNq; ++c) final_obs[kAntOb * i + c] = qpost[kAntNq * i + c];
+        for (int c = 0; c < kAntNv; ++c) final_obs[kAntOb * i + kAntNq + c] = vpost[kAntNv * i + c];
+      }
+      const uint64_t gi = (uint64_t)(i + P.env_base);
+      const uint32_t ep = S.episode[i] + 1u;
+      const int32_t task = S.task[i];
+      double r[4];
+      reset_draws(gi, ep, k0, k1, r);
+      double x, y, gx, gy;
+      reset_one(P, task, nullptr, r, x, y, gx, gy);
+      double q[kAntNq], v[kAntNv];
+      ant_reset_body(gi, ep, k0, k1, nullptr, reset_states ? reset_states + (int64_t)kAntOb * i : nullptr, x, y,
+                     q, v);
+      for (int c = 0; c < kAntNq; ++c) {
+        bq[kAntNq * i + c] = q[c];
+        obs[kAntOb * i + c] = q[c];
+      }
+      for (int c = 0; c < kAntNv; ++c) {
+        bv[kAntNv * i + c] = v[c];
+        obs[kAntOb * i + kAntNq + c] = v[c];
+      }
+      reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
+      S.episode[i] = ep;
+      el = 0;
+      nx = x;
+      ny = y;
+    }
+    reinterpret_cast<double2*>(S.qpos)[i] = make_double2(nx, ny);  // get_xy()
+    S.elapsed[i] = el;
+    kind_s[threadIdx.x] = kind;
+    xy_s[threadIdx.x] = make_double2(nx, ny);
+  }
+  __syncthreads();
+  // phase B stores
+  double* ob = obs + kAntOb * base;
+  double* bqb = bq + kAntNq * base;
+  double* bvb = bv + kAntNv * base;
+#pragma unroll
+  for (int r = 0; r < kAntPer; ++r) {
+    const int f = (int)threadIdx.x + kAntThreads * r;
+    if (f >= tot) continue;
+    const int e = f / kAntOb, c = f - e * kAntOb;
+    const uint8_t kind = kind_s[e];
+    if (kind == kRowReset) continue;  // written whole in phase A
+    ob[f] = val[r];
+    if (c < kAntNq) {
+      const bool tp = kind == kRowTeleport && c < 2;
+      if (!in_place || tp) bqb[kAntNq * e + c] = tp ? (c == 0 ? xy_s[e].x : xy_s[e].y) : val[r];
+    } else if (!in_place) {
+      bvb[kAntNv * e + (c - kAntNq)] = val[r];
+    }
+  }
+}
+
+}  // namespace ogbx

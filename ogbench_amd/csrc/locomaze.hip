@@ -73,6 +73,8 @@ struct ogbx_maze_env {
   int16_t* bfs = nullptr;  // [H*W goal cell][H*W cell] BFS distances (maze.py:517-536)
   uint64_t seed = 0;
   bool was_reset = false;
+  double* body_qpos = nullptr;  // ant handles: f64[N,15] (antmaze.h)
+  double* body_qvel = nullptr;  // ant handles: f64[N,14]
   int epw = 64;  // envs per 64-lane wave of the step/physics kernels
   int lds_pad = 0;  // dynamic LDS bytes requested per step/physics workgroup
 };
@@ -513,6 +515,12 @@ __global__ void set_goal_kernel(const MazeParams* __restrict__ Pp, MazeState S, 
   reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
 }
 
+}  // namespace ogbx
+
+#include "antmaze.h"
+
+namespace ogbx {
+
 // ------------------------------------------------------------- host tables
 
 struct MazeSpec {
@@ -703,6 +711,12 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
   if (herr == hipSuccess) herr = hipMalloc(&e->S.elapsed, n * sizeof(int32_t));
   if (herr == hipSuccess) herr = hipMalloc(&e->S.task, n * sizeof(int32_t));
   if (herr == hipSuccess) herr = hipMalloc(&e->S.episode, n * sizeof(uint32_t));
+  if (herr == hipSuccess && P.loco_type == 1) {
+    herr = hipMalloc(&e->body_qpos, n * kAntNq * sizeof(double));
+    if (herr == hipSuccess) herr = hipMalloc(&e->body_qvel, n * kAntNv * sizeof(double));
+    if (herr == hipSuccess) herr = hipMemset(e->body_qpos, 0, n * kAntNq * sizeof(double));
+    if (herr == hipSuccess) herr = hipMemset(e->body_qvel, 0, n * kAntNv * sizeof(double));
+  }
   std::vector<int16_t> bfs;
   build_bfs(P, bfs);
   if (herr == hipSuccess) herr = hipMalloc(&e->Pd, sizeof(MazeParams));
@@ -732,6 +746,8 @@ ogbx_status ogbx_maze_destroy(ogbx_maze_t e) {
   (void)hipFree(e->S.elapsed);
   (void)hipFree(e->S.task);
   (void)hipFree(e->S.episode);
+  (void)hipFree(e->body_qpos);
+  (void)hipFree(e->body_qvel);
   (void)hipFree(e->bfs);
   (void)hipFree(e->Pd);
   delete e;
@@ -814,6 +830,7 @@ ogbx_status ogbx_maze_reset(ogbx_maze_t e, const int32_t* task_id, const double*
                             uint64_t seed, void* stream) {
   OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
   OGBX_CHECK(obs != nullptr && goal != nullptr, OGBX_EINVAL, "ogbx_maze_reset: null output");
+  OGBX_CHECK(e->P.loco_type != 1, OGBX_EINVAL, "ant handles reset through ogbx_antmaze_reset");
   OGBX_HIP(hipSetDevice(e->device));
   e->seed = seed;
   uint32_t k0, k1;
@@ -851,6 +868,51 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
                        final_obs, auto_reset, k0, k1, epw, nullptr);
   OGBX_LAUNCHED("maze_step_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_antmaze_state(ogbx_maze_t e, double** body_qpos, double** body_qvel) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->P.loco_type == 1, OGBX_EINVAL, "ogbx_antmaze_state: not an ant handle");
+  if (body_qpos) *body_qpos = e->body_qpos;
+  if (body_qvel) *body_qvel = e->body_qvel;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_antmaze_reset(ogbx_maze_t e, const int32_t* task_id, const double* task_xy, const uint8_t* mask,
+                               const double* noise, const double* body_draws, double* obs, double* goal,
+                               uint64_t seed, void* stream) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->P.loco_type == 1, OGBX_EINVAL, "ogbx_antmaze_reset: not an ant handle");
+  OGBX_CHECK(obs != nullptr && goal != nullptr, OGBX_EINVAL, "ogbx_antmaze_reset: null output");
+  OGBX_HIP(hipSetDevice(e->device));
+  e->seed = seed;
+  uint32_t k0, k1;
+  seed_key(seed, kTagMazeReset, &k0, &k1);
+  hipLaunchKernelGGL(ant_reset_kernel, dim3(grid_for(e->n, 256)), dim3(256), 0, (hipStream_t)stream, e->Pd, e->S,
+                     e->body_qpos, e->body_qvel, e->n, task_id, task_xy, mask, noise, body_draws, obs, goal, k0, k1);
+  OGBX_LAUNCHED("ant_reset_kernel");
+  e->was_reset = true;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_antmaze_step(ogbx_maze_t e, const double* qpos_post, const double* qvel_post, double* obs,
+                              float* reward, uint8_t* terminated, uint8_t* truncated, uint8_t* success,
+                              double* final_obs, int32_t auto_reset, const double* reset_states, void* stream) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->P.loco_type == 1, OGBX_EINVAL, "ogbx_antmaze_step: not an ant handle");
+  OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
+  OGBX_CHECK(qpos_post && qvel_post && obs && reward && terminated && truncated && success, OGBX_EINVAL,
+             "ogbx_antmaze_step: null argument");
+  const bool qin = qpos_post == e->body_qpos, vin = qvel_post == e->body_qvel;
+  OGBX_CHECK(qin == vin, OGBX_EINVAL, "ogbx_antmaze_step: qpos and qvel must both be (or both not be) the handle's state");
+  OGBX_HIP(hipSetDevice(e->device));
+  uint32_t k0, k1;
+  seed_key(e->seed, kTagMazeReset, &k0, &k1);
+  hipLaunchKernelGGL(ant_step_kernel, dim3(grid_for(e->n, kAntEnvs)), dim3(kAntThreads), 0, (hipStream_t)stream, e->Pd, e->S,
+                     e->body_qpos, e->body_qvel, e->n, qpos_post, qvel_post, (int32_t)qin, obs, reward, terminated,
+                     truncated, success, final_obs, auto_reset, reset_states, k0, k1);
+  OGBX_LAUNCHED("ant_step_kernel");
   return OGBX_OK;
 }
 

@@ -163,9 +163,10 @@ class MazeEnv:
 
         n = self.num_envs
         kw = dict(device=self.device)
-        self._obs = torch.zeros(n, 2, dtype=torch.float64, **kw)
+        self._ob_dim = 2 if loco_env_type == 'point' else ob_dim
+        self._obs = torch.zeros(n, self._ob_dim, dtype=torch.float64, **kw)
         self._goal = torch.zeros(n, 2, dtype=torch.float64, **kw)
-        self._final_obs = torch.zeros(n, 2, dtype=torch.float64, **kw)
+        self._final_obs = torch.zeros(n, self._ob_dim, dtype=torch.float64, **kw)
         self._reward = torch.zeros(n, dtype=torch.float32, **kw)
         self._term = torch.zeros(n, dtype=torch.uint8, **kw)
         self._trunc = torch.zeros(n, dtype=torch.uint8, **kw)
@@ -306,8 +307,12 @@ class MazeEnv:
 
     def state_dict(self):
         q, g, e, t, ep = self._state_views()
-        return dict(qpos=q.clone(), goal=g.clone(), elapsed=e.clone(), task=t.clone(), episode=ep.clone(),
-                    seed=self._seed)
+        sd = dict(qpos=q.clone(), goal=g.clone(), elapsed=e.clone(), task=t.clone(), episode=ep.clone(),
+                  seed=self._seed)
+        if self._loco_env_type == 'ant':
+            bq, bv = self.body_state()
+            sd.update(body_qpos=bq.clone(), body_qvel=bv.clone())
+        return sd
 
     def load_state_dict(self, sd):
         q, g, e, t, ep = self._state_views()
@@ -317,6 +322,10 @@ class MazeEnv:
         t.copy_(sd['task'])
         if 'episode' in sd:
             ep.copy_(sd['episode'])
+        if self._loco_env_type == 'ant' and 'body_qpos' in sd:
+            bq, bv = self.body_state()
+            bq.copy_(sd['body_qpos'])
+            bv.copy_(sd['body_qvel'])
         if sd.get('seed') is not None:
             self._seed = int(sd['seed'])
         self._has_reset = True
@@ -349,9 +358,13 @@ class MazeEnv:
 
         options: ``task_id`` (int or [N] tensor), ``task_info`` (dict with
         init_ij/goal_ij, or an [N,4] xy tensor), ``noise`` ([N,4] injected
-        uniform(-1,1) draws; test hook), ``render_goal`` (unsupported).
-        Returns (obs [N,2] f64, {'goal': [N,2] f64}).
+        uniform(-1,1) draws; test hook), ``render_goal`` (unsupported); ant
+        handles also take ``body_draws`` ([N,29] injected AntEnv.reset_model
+        draws: 15 uniform(-0.1,0.1), 14 standard normal).
+        Returns (obs [N,2] f64 (point) | [N,29] f64 (ant), {'goal': [N,2] f64}).
         """
+        if self._loco_env_type == 'humanoid':
+            raise NotImplementedError('humanoid dynamics and its observation layout are out of scope')
         torch = _torch()
         options = {} if options is None else options
         if options.get('render_goal'):
@@ -383,6 +396,19 @@ class MazeEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask).to(self.device, torch.uint8).contiguous()
+        if self._loco_env_type == 'ant':
+            bd = options.get('body_draws')
+            if bd is not None:
+                bd = torch.as_tensor(bd).to(self.device, torch.float64).contiguous()
+                assert bd.shape == (self.num_envs, 29)
+            _lib.check(
+                self._L.ogbx_antmaze_reset(self._h, _lib.ptr(task_t), _lib.ptr(task_xy), _lib.ptr(m),
+                                           _lib.ptr(noise), _lib.ptr(bd), _lib.ptr(self._obs), _lib.ptr(self._goal),
+                                           self._seed, self._stream()),
+                'reset',
+            )
+            self._has_reset = True
+            return self._obs, {'goal': self._goal}
         _lib.check(
             self._L.ogbx_maze_reset(
                 self._h,
@@ -418,6 +444,10 @@ class MazeEnv:
         action: [N,2] float32 (NEP-50 float32 scaling) or float64.
         Returns (obs, reward, terminated, truncated, info) with info['success'].
         """
+        if self._loco_env_type != 'point':
+            raise NotImplementedError(
+                f'{self._loco_env_type} dynamics are out of scope: advance body_state() with your physics engine '
+                'and call wrap_step(qpos, qvel)')
         a = self._action(action)
         if a.shape != (self.num_envs, 2):
             raise ValueError(f'action must have shape ({self.num_envs}, 2), got {tuple(a.shape)}')
@@ -426,6 +456,48 @@ class MazeEnv:
                 self._h, a.data_ptr(), int(a.dtype == _torch().float64), 1, *self._step_out,
                 int(self.auto_reset), self._stream()),
             'step',
+        )
+        info = {'success': self._succ_b}
+        if self.auto_reset:
+            info['final_observation'] = self._final_obs
+        return self._obs, self._reward, self._term_b, self._trunc_b, info
+
+    # ------------------------------------------------------------ antmaze wrapper
+    def body_state(self):
+        """Ant handles: device views (qpos f64[N,15], qvel f64[N,14]) of the body
+        state -- what a physics engine reads and overwrites in place."""
+        torch = _torch()
+        if self._loco_env_type != 'ant':
+            raise ValueError('body_state() is for ant handles')
+        q, v = _lib.c_void_p(), _lib.c_void_p()
+        _lib.check(self._L.ogbx_antmaze_state(self._h, q, v))
+        n = self.num_envs
+        return (_from_ptr(q.value, (n, 15), torch.float64, self.device),
+                _from_ptr(v.value, (n, 14), torch.float64, self.device))
+
+    def wrap_step(self, qpos, qvel, reset_states=None):
+        """MazeEnv.step + TimeLimit (maze.py:433-466) around caller-supplied ant
+        physics: qpos [N,15] / qvel [N,14] f64 = the post-physics state (the
+        tensors of body_state(), stepped in place, or any other buffers).
+
+        Returns (obs [N,29], reward, terminated, truncated, info{'success'}) as
+        ``step`` does; with auto_reset, ``reset_states`` [N,29] (optional) are
+        the caller's reset states for the envs that end (xy := init_xy)."""
+        torch = _torch()
+        if self._loco_env_type != 'ant':
+            raise ValueError('wrap_step() is for ant handles; point envs use step(action)')
+        q = qpos if qpos.is_contiguous() else qpos.contiguous()
+        v = qvel if qvel.is_contiguous() else qvel.contiguous()
+        assert q.dtype == torch.float64 and v.dtype == torch.float64 and q.device == self.device
+        assert q.shape == (self.num_envs, 15) and v.shape == (self.num_envs, 14)
+        rs = None
+        if reset_states is not None:
+            rs = torch.as_tensor(reset_states).to(self.device, torch.float64).contiguous()
+            assert rs.shape == (self.num_envs, 29)
+        _lib.check(
+            self._L.ogbx_antmaze_step(self._h, _lib.ptr(q), _lib.ptr(v), *self._step_out[:5],
+                                      self._step_out[5], int(self.auto_reset), _lib.ptr(rs), self._stream()),
+            'wrap_step',
         )
         info = {'success': self._succ_b}
         if self.auto_reset:

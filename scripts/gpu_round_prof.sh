@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-WLS=${WLS:-"pointmaze powder powder-medium powder-hard gcsample hgcsample"}
+WLS=${WLS:-"pointmaze powder powder-medium powder-hard gcsample hgcsample antmaze"}
 for wl in $WLS; do
   case $wl in
     pointmaze) K=maze_step_kernel; S=2000 ;;
@@ -12,6 +12,7 @@ for wl in $WLS; do
     powder-medium|powder-hard) K=pwf_light_step_kernel+pwf_step_kernel; S=600 ;;
     gcsample) K=gc_sample_kernel; S=300 ;;
     hgcsample) K=hgc_sample_kernel; S=300 ;;
+    antmaze) K=ant_step_kernel; S=2000 ;;
     *) echo "unknown workload $wl"; exit 2 ;;
   esac
   WL=$wl KERNEL=$K STEPS=$S bash scripts/gpu_prof.sh || exit $?

@@ -1,0 +1,150 @@
+"""GPU parity: the antmaze wrapper (loco_type 'ant', ogbx_antmaze_* through the
+C-ABI) vs the reference's own MazeEnv/AntEnv methods.
+
+tests/golden/antmaze_golden.npz (tests/golden/make_golden_ant.py) holds, for
+success_timing 'post' and 'pre', 24 antmaze-large envs reset with recorded
+draws (add_noise's np.random.uniform, AntEnv.reset_model's np_random uniform /
+standard_normal) and stepped 40 times on given post-physics states under a
+TimeLimit of 30: the reference's ob, reward, terminated, truncated and
+success.  All bit-exact.  The ant's articulated dynamics are out of scope (and
+unpinned): the fixture's post-physics states stand in for them.
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import ogbench_amd
+from oracle import locomaze as orc
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'antmaze_golden.npz')
+
+
+@pytest.fixture(scope='module')
+def golden():
+    return dict(np.load(GOLDEN))
+
+
+def _env(gpu, n, timing, **kw):
+    return ogbench_amd.MazeEnv('ant', 'large', num_envs=n, device=gpu, success_timing=timing, **kw)
+
+
+@pytest.mark.parametrize('timing', ['post', 'pre'])
+@pytest.mark.parametrize('in_place', [False, True])
+def test_wrapper_matches_reference(gpu, golden, timing, in_place):
+    g = {k[len(timing) + 1:]: v for k, v in golden.items() if k.startswith(timing + '_')}
+    n = g['task'].shape[0]
+    env = _env(gpu, n, timing, max_episode_steps=int(golden['max_episode_steps']))
+    obs, info = env.reset(seed=0, options=dict(task_id=torch.tensor(g['task']), noise=torch.tensor(g['noise']),
+                                               body_draws=torch.tensor(g['body_draws'])))
+    assert obs.shape == (n, 29)
+    assert np.array_equal(obs.cpu().numpy(), g['reset_obs'])
+    assert np.array_equal(info['goal'].cpu().numpy(), g['reset_goal'])
+    bq, bv = env.body_state()
+    for t in range(g['obs'].shape[0]):
+        q = torch.tensor(g['qpos_post'][t], device=gpu)
+        v = torch.tensor(g['qvel_post'][t], device=gpu)
+        if in_place:  # the physics engine overwrote the handle's state
+            bq.copy_(q)
+            bv.copy_(v)
+            q, v = bq, bv
+        o, r, te, tr, inf = env.wrap_step(q, v)
+        assert np.array_equal(o.cpu().numpy(), g['obs'][t]), t
+        assert np.array_equal(r.cpu().numpy(), g['reward'][t]), t
+        assert np.array_equal(te.cpu().numpy(), g['terminated'][t].astype(bool)), t
+        assert np.array_equal(tr.cpu().numpy(), g['truncated'][t].astype(bool)), t
+        assert np.array_equal(inf['success'].cpu().numpy(), g['success'][t].astype(bool)), t
+        # the body state is the post-physics state (no teleport in this maze)
+        assert np.array_equal(bq.cpu().numpy(), g['qpos_post'][t])
+        assert np.array_equal(bv.cpu().numpy(), g['qvel_post'][t])
+        assert np.array_equal(env.get_xy().cpu().numpy(), g['qpos_post'][t][:, :2])
+    assert g['terminated'].sum() > 50 and g['truncated'].sum() > 50
+
+
+def test_auto_reset_with_caller_reset_states(gpu):
+    """Same-step auto-reset: the ending envs take the caller's reset state rows
+    with xy := init_xy (Philox xy draws of the handle's seed, as the point env),
+    obs is the new ob, final_observation the pre-reset ob."""
+    n, seed = 512, 77
+    env = _env(gpu, n, 'post', auto_reset=True, max_episode_steps=3)
+    tid = (np.arange(n) % 5 + 1).astype(np.int32)
+    env.reset(seed=seed, options=dict(task_id=torch.tensor(tid)))
+    rng = np.random.RandomState(3)
+    tables = np.array([list(t['init_xy']) + list(t['goal_xy']) for t in env.task_infos])
+    for t in range(3):
+        q = torch.tensor(rng.normal(size=(n, 15)) + 100.0, device=gpu)  # far from every goal
+        v = torch.tensor(rng.normal(size=(n, 14)), device=gpu)
+        rs = rng.normal(size=(n, 29))
+        o, r, te, tr, info = env.wrap_step(q, v, reset_states=torch.tensor(rs, device=gpu))
+        if t < 2:
+            assert not tr.any() and np.array_equal(o.cpu().numpy(), np.concatenate([q.cpu(), v.cpu()], 1))
+            continue
+        assert tr.all() and not te.any()
+        draws = orc.reset_draws(n, seed, env_base=0, episode=2)  # episode counter after this reset
+        init = tables[tid - 1, :2] + draws[:, :2] * 4.0 / 4.0
+        goal = tables[tid - 1, 2:] + draws[:, 2:] * 4.0 / 4.0
+        exp = rs.copy()
+        exp[:, :2] = init
+        assert np.array_equal(o.cpu().numpy(), exp)
+        assert np.array_equal(info['final_observation'].cpu().numpy(), np.concatenate([q.cpu(), v.cpu()], 1))
+        assert np.array_equal(env.cur_goal_xy.cpu().numpy(), goal)
+        bq, bv = env.body_state()
+        assert np.array_equal(bq.cpu().numpy(), exp[:, :15]) and np.array_equal(bv.cpu().numpy(), exp[:, 15:])
+
+
+def test_philox_reset_body_distribution(gpu):
+    """Without injected draws: qpos = qpos0 + U(-0.1, 0.1) (xy := init_xy),
+    qvel = 0.1 N(0, 1); deterministic per (seed, global env)."""
+    n = 1 << 16
+    env = _env(gpu, n, 'post')
+    obs = env.reset(seed=5, options=dict(task_id=1))[0].cpu().numpy()
+    q0 = np.array([0, 0, 0.75, 1, 0, 0, 0] + [0] * 8, np.float64)
+    dq = obs[:, 2:15] - q0[2:]
+    assert np.abs(dq).max() <= 0.1 and abs(dq.mean()) < 2e-3 and abs(dq.std() - 0.2 / np.sqrt(12)) < 2e-3
+    z = obs[:, 15:] / 0.1
+    assert abs(z.mean()) < 5e-3 and abs(z.std() - 1.0) < 5e-3
+    init = np.array(env.task_infos[0]['init_xy'])
+    assert np.abs(obs[:, :2] - init).max() <= 1.0
+    half = _env(gpu, n // 2, 'post', env_base=n // 2)
+    obs2 = half.reset(seed=5, options=dict(task_id=1))[0].cpu().numpy()
+    assert np.array_equal(obs2, obs[n // 2:])
+
+
+def test_teleport_moves_body_xy(gpu):
+    """antmaze-teleport: a post-physics xy inside an in-portal moves qpos[:2] to
+    the Philox-drawn out-portal (maze.py:442-451); ob keeps the pre-teleport xy."""
+    n, seed = 256, 9
+    env = ogbench_amd.MazeEnv('ant', 'teleport', num_envs=n, device=gpu)
+    env.reset(seed=seed, options=dict(task_id=2))
+    rng = np.random.RandomState(1)
+    q = rng.normal(size=(n, 15))
+    q[:, :2] = np.array([20.0, 12.0]) + rng.uniform(-1.2, 1.2, (n, 2))  # in-portal (4, 6) at (20, 12), r 1.5
+    v = rng.normal(size=(n, 14))
+    o, *_ = env.wrap_step(torch.tensor(q, device=gpu), torch.tensor(v, device=gpu))
+    assert np.array_equal(o.cpu().numpy()[:, :2], q[:, :2])
+    xy = env.get_xy().cpu().numpy()
+    inside = np.hypot(q[:, 0] - 20.0, q[:, 1] - 12.0) <= 1.5
+    outs = np.array([[24.0, 0.0], [0.0, 20.0], [36.0, 20.0]])  # (1,7), (6,1), (6,10)
+    k0, k1 = orc.philox_key(seed, orc.TAG_MAZE_RESET)
+    for i in range(n):
+        if not inside[i]:
+            assert np.array_equal(xy[i], q[i, :2])
+            continue
+        w = orc.philox4x32([i, 1, 0x100, 0], k0 ^ 0x4D5A0002, k1)
+        o_idx = (int(w[0]) * 3) >> 32
+        assert np.array_equal(xy[i], outs[o_idx]), i
+    assert inside.sum() > 100
+    bq, _ = env.body_state()
+    assert np.array_equal(bq.cpu().numpy()[:, :2], xy)
+
+
+def test_point_only_entry_points_refuse_ant(gpu):
+    env = _env(gpu, 4, 'post')
+    env.reset(seed=0)
+    with pytest.raises(NotImplementedError):
+        env.step(torch.zeros(4, 8))
+    with pytest.raises(ValueError):
+        ogbench_amd.MazeEnv('point', 'large', num_envs=4, device=gpu).body_state()
