@@ -230,10 +230,13 @@ __global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __res
 // One launch = k_steps consecutive env steps of every env; state stays in
 // registers across the k loop.  One lane per env.
 // kUntilDone (no auto-reset): an env stops at the first step that ends its
-// episode (terminated | truncated); its later rows are not written and
-// steps_taken[i] counts the rows it wrote.  A wave leaves the k loop as soon as
-// a ballot finds every lane done, so a batch of evaluation episodes costs the
-// steps of its longest episode per wave, not k_steps.
+// episode (terminated | truncated); its later rows are not written, its state
+// is the state at that step, and steps_taken[i] counts the rows it wrote.  A
+// wave leaves the k loop as soon as a ballot finds every lane done, so a batch
+// of evaluation episodes costs the steps of its longest episode per wave, not
+// k_steps.  Until then a done lane keeps stepping unobserved (as K single
+// steps would), so the wave's contact-path choice -- and with it every written
+// row -- is bit-identical to K calls of the single step.
 template <bool kF64, bool kUntilDone>
 __global__ void __launch_bounds__(256) maze_step_kernel(
     const MazeParams* __restrict__ Pp, MazeState S, int64_t n, const void* __restrict__ action_v,
@@ -270,11 +273,12 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
   bool reset_any = false;  // goal / episode change only on an auto-reset
   bool done = false;       // kUntilDone: this env's episode has ended
   int32_t taken = 0;
+  double dx_ = x, dy_ = y;  // kUntilDone: the state at the end of the episode
+  int32_t del_ = el;
 
   for (int32_t k = 0; k < k_steps; ++k) {
     if (kUntilDone) {
       if (__all(done)) break;  // wave-uniform early exit (ballot over live lanes)
-      if (done) continue;
     }
     const int64_t o = (int64_t)k * n + i;
     double dx, dy;
@@ -311,10 +315,13 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     const bool term = succ && P.terminate_at_goal;
     el += 1;
     const bool trunc = el >= P.max_steps;
-    reward[o] = rew;
-    terminated[o] = term;
-    truncated[o] = trunc;
-    success[o] = succ;
+    const bool write = !kUntilDone || !done;
+    if (write) {
+      reward[o] = rew;
+      terminated[o] = term;
+      truncated[o] = trunc;
+      success[o] = succ;
+    }
     double wx = ox, wy = oy;
     if (auto_reset && (term || trunc)) {
       if (final_obs != nullptr) reinterpret_cast<double2*>(final_obs)[o] = make_double2(ox, oy);
@@ -327,15 +334,23 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
       wx = x;
       wy = y;
     }
-    reinterpret_cast<double2*>(obs)[o] = make_double2(wx, wy);
-    if (kUntilDone) {
+    if (write) reinterpret_cast<double2*>(obs)[o] = make_double2(wx, wy);
+    if (kUntilDone && !done) {
       taken = k + 1;
       done = term || trunc;
+      dx_ = x;
+      dy_ = y;
+      del_ = el;
     }
+  }
+  if (kUntilDone) {
+    x = dx_;
+    y = dy_;
+    el = del_;
+    steps_taken[i] = taken;
   }
   reinterpret_cast<double2*>(S.qpos)[i] = make_double2(x, y);
   S.elapsed[i] = el;
-  if (kUntilDone) steps_taken[i] = taken;
   if (reset_any) {
     reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
     S.episode[i] = ep;

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_locomaze_gpu.py tests/test_shard_gpu.py -m gpu -x -q --timeout 200 \
+timeout -k 10 300 python -u -m pytest tests/test_locomaze_gpu.py tests/test_contact_pin_gpu.py tests/test_shard_gpu.py -m gpu -x -q --timeout 200 \
   --timeout-method thread > gpurun_out/quick_pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/quick_pytest.log; [ $rc -eq 0 ] || exit $rc
 for N in 65536 8192; do
