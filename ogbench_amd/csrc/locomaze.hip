@@ -263,11 +263,23 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     q = reinterpret_cast<const double2*>(S.qpos)[i];
     g = reinterpret_cast<const double2*>(S.goal)[i];
     el = S.elapsed[i];
-    ep = S.episode[i];
-    task = S.task[i];
   }
   nbmask_commit(nb_s, nbv);
   if (!live) return;
+  // task and episode counter are read only by an auto-reset or a teleport:
+  // fetched here (their round trip hides under the physics) for the envs that
+  // can end this step -- TimeLimit, or within goal_tol + 2 of the goal (a step
+  // moves |0.2 a| <= 0.29 for actions in the action space) -- and lazily by
+  // any other env that does end (an out-of-space action)
+  bool have_te = k_steps > 1 || P.n_tp_in > 0 || el + 1 >= P.max_steps;
+  {
+    const double ddx = q.x - g.x, ddy = q.y - g.y, lim = P.goal_tol + 2.0;
+    have_te |= ddx * ddx + ddy * ddy <= lim * lim;
+  }
+  if (have_te) {
+    ep = S.episode[i];
+    task = S.task[i];
+  }
   const uint64_t gi = (uint64_t)(i + P.env_base);
   double x = q.x, y = q.y, gx = g.x, gy = g.y;
   bool reset_any = false;  // goal / episode change only on an auto-reset
@@ -324,6 +336,11 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     }
     double wx = ox, wy = oy;
     if (auto_reset && (term || trunc)) {
+      if (!have_te) {
+        ep = S.episode[i];
+        task = S.task[i];
+        have_te = true;
+      }
       if (final_obs != nullptr) reinterpret_cast<double2*>(final_obs)[o] = make_double2(ox, oy);
       ep += 1u;
       reset_any = true;
