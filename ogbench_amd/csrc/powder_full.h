@@ -56,6 +56,7 @@ struct alignas(16) PwFullShared {
   int32_t elem_ids[8];
   float vel_q[8];  // angle-bin thresholds on q (PowderParams::vel_q)
   int32_t red[16];
+  uint64_t rowm[3][WS];  // per-row cell bitmasks (bit c = column c) of rule predicates
 };
 
 // render colours as float32 c / 255 (sim.py:402-453), velocity colour
@@ -161,6 +162,41 @@ struct FullWorld {
       n += ((j >= 0) & pred(fid(x))) ? 1 : 0;
     }
     return n;
+  }
+
+  // Per-row bitmasks of a cell predicate: a wave holds whole rows, so one
+  // ballot per row and slab gives the row's mask; the row masks go to LDS and
+  // every cell answers "how many / any X in my zero-padded 3x3" from the three
+  // rows' masks with shifts and popcounts -- uniform across the wave, where
+  // the per-cell box() loops and the scatter dilations ran divergent
+  // few-lane loops.  Call with every thread; a sync() must separate the
+  // writes from the reads.
+  template <typename P>
+  __device__ __forceinline__ void row_masks(uint64_t* rm, P pred) const {
+    const int lane = (int)(threadIdx.x & 63u);
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const uint64_t b = __ballot(pred(k));
+      if (W == 64) {
+        if (lane == 0) rm[row(k)] = b;
+      } else {  // W = 32: lanes 0-31 hold one row, lanes 32-63 the next
+        if ((lane & 31) == 0) rm[row(k)] = lane == 0 ? (b & 0xFFFFFFFFull) : (b >> 32);
+      }
+    }
+  }
+  // bits (c-1, c, c+1) of row r's mask, zero outside the world
+  __device__ __forceinline__ uint32_t win3(const uint64_t* rm, int r) const {
+    if ((unsigned)r >= (unsigned)H) return 0u;
+    const uint64_t x = rm[r];
+    return (uint32_t)((col == 0 ? x << 1 : x >> (col - 1)) & 7u);
+  }
+  __device__ __forceinline__ int count3x3(const uint64_t* rm, int k) const {
+    const int r = row(k);
+    return __popc(win3(rm, r - 1)) + __popc(win3(rm, r)) + __popc(win3(rm, r + 1));
+  }
+  __device__ __forceinline__ bool any3x3(const uint64_t* rm, int k) const {
+    const int r = row(k);
+    return (win3(rm, r - 1) | win3(rm, r) | win3(rm, r + 1)) != 0u;
   }
 
   // ------------------------------------------------------------- rules
@@ -377,11 +413,16 @@ struct FullWorld {
     asm volatile("; ICE_BEGIN");
 #endif
     fence_idx();
+    uint64_t* melt = s.rowm[0];  // empty | fire | lava | water
+    row_masks(melt, [&](int k) {
+      const uint32_t x = fid(s.a[cell(k)]);
+      return x == kEmpty || x == kFire || x == kLava || x == kWater;
+    });
+    sync();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
-      bool to = id == kIce && ri_lt(k, kRi002);
-      if (to) to = box(k, [](uint32_t x) { return x == kEmpty || x == kFire || x == kLava || x == kWater; }) > 1;
+      const bool to = (id == kIce) & ri_lt(k, kRi002) & (count3x3(melt, k) > 1);
       s.f1[cell(k)] = to ? kWater + 1 : 0;
     }
     commit_conversions();
@@ -389,11 +430,13 @@ struct FullWorld {
 
   __device__ __forceinline__ void water() const {
     fence_idx();
+    uint64_t* ice = s.rowm[0];
+    row_masks(ice, [&](int k) { return fid(s.a[cell(k)]) == kIce; });
+    sync();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
-      bool to = id == kWater && re_lt(k, kRe005);
-      if (to) to = box(k, [](uint32_t x) { return x == kIce; }) >= 3;
+      const bool to = (id == kWater) & re_lt(k, kRe005) & (count3x3(ice, k) >= 3);
       s.f1[cell(k)] = to ? kIce + 1 : 0;
     }
     commit_conversions();
@@ -404,38 +447,26 @@ struct FullWorld {
            x == kMole || x == kLemming;
   }
 
-  // BehaviorFire (sim.py:700-790).  Fire and lava are sparse, so the two
-  // "is there X in my 3x3" questions are answered by dilation: the few source
-  // cells mark their 3x3 neighbourhood in a flag array (benign same-value
-  // stores) and every cell reads its own flag.  The burnable-neighbour counts
-  // are evaluated only for the cells whose outcome depends on them (cells
-  // that were fire/lava, fire that may fade, empty cells that ignite).
+  // BehaviorFire (sim.py:700-790).  The "is there X in my 3x3" and "how
+  // many burnable cells in my 3x3" questions are answered from per-row
+  // bitmasks (row_masks): fire|lava before the burn, the burnable cells after
+  // it, and the spread sources.
   __device__ __forceinline__ void fire() const {
 #ifdef OGBX_ASM_MARKS
     asm volatile("; FIRE_BEGIN");
 #endif
     static_assert(CPT <= 4, "conversion codes packed 8 bits per cell");
     fence_idx();
-    uint8_t* near = s.f1;  // 3x3 dilation of fire|lava before the burn
-    int8_t* hot = s.sw;    // 3x3 dilation of the cells that spread fire
-    uint32_t flb = 0;      // bit k: this cell was fire or lava before the burn
+    uint64_t* hotm = s.rowm[0];   // fire | lava before the burn
+    uint64_t* burnm = s.rowm[1];  // burnable cells after the burn
+    uint64_t* srcm = s.rowm[2];   // fire spread sources
+    uint32_t flb = 0;             // bit k: this cell was fire or lava before the burn
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const uint32_t id = fid(s.a[i]);
-      near[i] = 0;
-      hot[i] = 0;
+      const uint32_t id = fid(s.a[cell(k)]);
       flb |= (id == kFire || id == kLava) ? 1u << k : 0u;
     }
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k)
-      if ((flb >> k) & 1u)
-#pragma unroll 1
-        for (int q = 0; q < 9; ++q) {
-          const int j = zp(k, q / 3 - 1, q % 3 - 1);
-          if (j >= 0) near[j] = 1;
-        }
+    row_masks(hotm, [&](int k) { return ((flb >> k) & 1u) != 0u; });
     sync();
     // burn decisions; f2 bit 0: burns (pushes its 4 neighbours with 8), bit 1:
     // dust near fire (pushes with 30)
@@ -444,7 +475,7 @@ struct FullWorld {
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t id = fid(s.a[i]);
-      const bool nr = near[i];
+      const bool nr = any3x3(hotm, k);
       const bool p005 = ri_lt(k, kRi005), p02 = ri_lt(k, kRi02);
       const bool cand = (id == kWood && p005) | (id == kPlant && p02) | (id == kGas && p02) | (id == kDust) |
                         (id == kBird && p005) |
@@ -477,39 +508,35 @@ struct FullWorld {
       }
     }
     sync();
+    // burnable neighbour counts on the post-burn world
+    row_masks(burnm, [&](int k) { return burnable(fid(s.a[cell(k)])); });
+    sync();
     // fire spread sources: (fire or lava before the burn) with a burnable
     // neighbour, and lava; fading fire (no burnable neighbour)
     uint32_t fade = 0;
+    int nbr[CPT];
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const uint32_t id = fid(s.a[i]);
-      const bool fl = (flb >> k) & 1u;
-      const bool re04 = re_lt(k, kRe04);
-      const bool need = fl | ((id == kFire) & re04);
-      const int nbr = need ? box(k, [](uint32_t x) { return burnable(x); }) : 1;
-      if ((fl & (nbr > 0)) | (id == kLava))
-#pragma unroll 1
-        for (int q = 0; q < 9; ++q) {
-          const int j = zp(k, q / 3 - 1, q % 3 - 1);
-          if (j >= 0) hot[j] = 1;
-        }
-      fade |= ((id == kFire) & re04 & (nbr == 0)) ? 1u << k : 0u;
+      const uint32_t id = fid(s.a[cell(k)]);
+      nbr[k] = count3x3(burnm, k);
+      fade |= ((id == kFire) & re_lt(k, kRe04) & (nbr[k] == 0)) ? 1u << k : 0u;
     }
+    row_masks(srcm, [&](int k) {
+      const bool fl = (flb >> k) & 1u;
+      return (fl & (nbr[k] > 0)) | (fid(s.a[cell(k)]) == kLava);
+    });
     sync();
     // empty cells next to a source ignite (ri < 0.3); fire with re < 0.4 and
     // no burnable neighbour fades to empty (sim.py:778-790)
     uint32_t conv2 = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const uint32_t id = fid(s.a[i]);
-      const bool burn_empty = (id == kEmpty) & ri_lt(k, kRi03) & (hot[i] != 0);
+      const uint32_t id = fid(s.a[cell(k)]);
+      const bool burn_empty = (id == kEmpty) & ri_lt(k, kRi03) & any3x3(srcm, k);
       bool fd = (fade >> k) & 1u;
-      if (burn_empty && re_lt(k, kRe04)) fd = box(k, [](uint32_t x) { return burnable(x); }) == 0;
+      if (burn_empty & re_lt(k, kRe04)) fd = nbr[k] == 0;
       conv2 |= (fd ? kEmpty + 1u : (burn_empty ? kFire + 1u : 0u)) << (8 * k);
     }
-    sync();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t to = (conv2 >> (8 * k)) & 0xFFu;
@@ -523,19 +550,24 @@ struct FullWorld {
     asm volatile("; PLANT_BEGIN");
 #endif
     fence_idx();
+    uint64_t* plm = s.rowm[0];  // plant
+    uint64_t* iwm = s.rowm[1];  // ice | wood
+    row_masks(plm, [&](int k) { return fid(s.a[cell(k)]) == kPlant; });
+    row_masks(iwm, [&](int k) {
+      const uint32_t x = fid(s.a[cell(k)]);
+      return x == kIce || x == kWood;
+    });
+    sync();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
       const bool grow = id == kWater && ri_lt(k, kRi005);
       const bool seed = id == kEmpty && ri_lt(k, kRi02);
-      int to = 0;
-      if (grow || seed) {  // the only cells whose outcome depends on the neighbourhood
-        const int cnt = box(k, [](uint32_t x) { return x == kPlant; });
-        bool to_plant = grow && cnt <= 3 && cnt >= 1;
-        const bool to_empty = grow && cnt > 3;
-        if (seed && cnt > 0) to_plant = box(k, [](uint32_t x) { return x == kIce || x == kWood; }) > 0;
-        to = to_plant ? kPlant + 1 : (to_empty ? kEmpty + 1 : 0);
-      }
+      const int cnt = count3x3(plm, k);
+      bool to_plant = grow && cnt <= 3 && cnt >= 1;
+      const bool to_empty = grow && cnt > 3;
+      if (seed && cnt > 0) to_plant = any3x3(iwm, k);
+      const int to = to_plant ? kPlant + 1 : (to_empty ? kEmpty + 1 : 0);
       s.f1[cell(k)] = (uint8_t)to;
     }
     commit_conversions();
