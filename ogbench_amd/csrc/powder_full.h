@@ -691,31 +691,53 @@ struct FullWorld {
       });
     }
     // decay (x0.95) fused into the 3x3 blur (zero padded) of the decayed
-    // field, NumPy's einsum summation order
+    // field, NumPy's einsum summation order.  A wave holds whole rows: each
+    // cell loads its own column of rows r-1, r, r+1 (3 LDS reads instead of
+    // 9) and takes the column neighbours' taps from the adjacent lanes with
+    // DPP wave shifts (zero outside the row); the results stay in registers
+    // until every thread has read the field.
     if (!(kVelParts & 2)) return;
     const float w18 = 1.0f / 18.0f;
     fence_idx();
+    float2 res[CPT];
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
+      const int r = row(k);
+      const float2 z = make_float2(0.f, 0.f);
+      const float2 vu0 = s.v[((r - 1) & (H - 1)) * W + col], vm = s.v[r * W + col],
+                   vd0 = s.v[((r + 1) & (H - 1)) * W + col];
+      const float2 vu = r > 0 ? vu0 : z, vd = r < H - 1 ? vd0 : z;
       float tx[9], ty[9];
+      tx[1] = (vu.x * 0.95f) * w18, ty[1] = (vu.y * 0.95f) * w18;
+      tx[4] = (vm.x * 0.95f) * w18, ty[4] = (vm.y * 0.95f) * w18;
+      tx[7] = (vd.x * 0.95f) * w18, ty[7] = (vd.y * 0.95f) * w18;
 #pragma unroll
-      for (int q = 0; q < 9; ++q) {
-        const int j = zp(k, q / 3 - 1, q % 3 - 1);
-        const float2 v = j >= 0 ? s.v[j] : make_float2(0.f, 0.f);
-        tx[q] = (v.x * 0.95f) * w18;
-        ty[q] = (v.y * 0.95f) * w18;
+      for (int q = 1; q < 9; q += 3) {
+        tx[q - 1] = col_prev(tx[q]), ty[q - 1] = col_prev(ty[q]);
+        tx[q + 1] = col_next(tx[q]), ty[q + 1] = col_next(ty[q]);
       }
-      float2 own = s.v[cell(k)];
+      float2 own = vm;
       own.x = own.x * 0.95f;
       own.y = own.y * 0.95f;
       const float bx = (((tx[4] + tx[0]) + tx[8]) + (tx[5] + tx[1])) + ((tx[6] + tx[2]) + (tx[7] + tx[3]));
       const float by = (((ty[4] + ty[0]) + ty[8]) + (ty[5] + ty[1])) + ((ty[6] + ty[2]) + (ty[7] + ty[3]));
-      s.v2[cell(k)] = make_float2(bx + own.x * 0.5f, by + own.y * 0.5f);
+      res[k] = make_float2(bx + own.x * 0.5f, by + own.y * 0.5f);
     }
     sync();
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) s.v[cell(k)] = s.v2[cell(k)];
+    for (int k = 0; k < CPT; ++k) s.v[cell(k)] = res[k];
     sync();
+  }
+
+  // The value at column col - 1 / col + 1 of the same row (a wave holds whole
+  // rows: DPP wave_shr / wave_shl by one lane), +0 outside the world.
+  __device__ __forceinline__ float col_prev(float x) const {
+    const float y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x138, 0xF, 0xF, true));
+    return col == 0 ? 0.0f : y;
+  }
+  __device__ __forceinline__ float col_next(float x) const {
+    const float y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xF, 0xF, true));
+    return col == W - 1 ? 0.0f : y;
   }
 
   // ------------------------------------------------------------- env helpers
