@@ -195,8 +195,21 @@ struct FullWorld {
     return __popc(win3(rm, r - 1)) + __popc(win3(rm, r)) + __popc(win3(rm, r + 1));
   }
   __device__ __forceinline__ bool any3x3(const uint64_t* rm, int k) const {
-    const int r = row(k);
-    return (win3(rm, r - 1) | win3(rm, r) | win3(rm, r + 1)) != 0u;
+    if constexpr (W == 64) {
+      // the wave holds exactly row(k): dilate the three row masks once, in
+      // scalar registers, and test the lane's column bit
+      const int r = __builtin_amdgcn_readfirstlane(row(k));
+      uint64_t x = rm[r];
+      if (r > 0) x |= rm[r - 1];
+      if (r < H - 1) x |= rm[r + 1];
+      x = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+      const uint64_t d = x | (x << 1) | (x >> 1);
+      return (d >> col) & 1u;
+    } else {
+      const int r = row(k);
+      return (win3(rm, r - 1) | win3(rm, r) | win3(rm, r + 1)) != 0u;
+    }
   }
 
   // ------------------------------------------------------------- rules
@@ -513,17 +526,17 @@ struct FullWorld {
     sync();
     // fire spread sources: (fire or lava before the burn) with a burnable
     // neighbour, and lava; fading fire (no burnable neighbour)
-    uint32_t fade = 0;
-    int nbr[CPT];
+    uint32_t fade = 0, nbr = 0;  // bit k: some burnable cell in the 3x3
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
-      nbr[k] = count3x3(burnm, k);
-      fade |= ((id == kFire) & re_lt(k, kRe04) & (nbr[k] == 0)) ? 1u << k : 0u;
+      const bool b = any3x3(burnm, k);
+      nbr |= b ? 1u << k : 0u;
+      fade |= ((id == kFire) & re_lt(k, kRe04) & !b) ? 1u << k : 0u;
     }
     row_masks(srcm, [&](int k) {
       const bool fl = (flb >> k) & 1u;
-      return (fl & (nbr[k] > 0)) | (fid(s.a[cell(k)]) == kLava);
+      return (fl & ((nbr >> k) & 1u)) | (fid(s.a[cell(k)]) == kLava);
     });
     sync();
     // empty cells next to a source ignite (ri < 0.3); fire with re < 0.4 and
@@ -534,7 +547,7 @@ struct FullWorld {
       const uint32_t id = fid(s.a[cell(k)]);
       const bool burn_empty = (id == kEmpty) & ri_lt(k, kRi03) & any3x3(srcm, k);
       bool fd = (fade >> k) & 1u;
-      if (burn_empty & re_lt(k, kRe04)) fd = nbr[k] == 0;
+      if (burn_empty & re_lt(k, kRe04)) fd = !((nbr >> k) & 1u);
       conv2 |= (fd ? kEmpty + 1u : (burn_empty ? kFire + 1u : 0u)) << (8 * k);
     }
 #pragma unroll
