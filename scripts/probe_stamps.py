@@ -1,6 +1,6 @@
 """Diagnostic: per-wave (max over lanes) cycle split of point_step
 (collide / solve / update) on realistic states: a warmed-up pointmaze-large
-rollout.  Run with OGBX_LIB=build/variants/libogbx_stamps.so."""
+rollout.  Run with OGBX_LIB=<a -DOGBX_PHYS_STAMPS build>."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, ogbench_amd
