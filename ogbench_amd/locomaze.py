@@ -175,6 +175,7 @@ class MazeEnv:
         self._step_out = (_lib.ptr(self._obs), _lib.ptr(self._reward), _lib.ptr(self._term),
                           _lib.ptr(self._trunc), _lib.ptr(self._succ),
                           _lib.ptr(self._final_obs))  # written only by an auto-reset
+        self._ant_qshape, self._ant_vshape, self._f64 = torch.Size((n, 15)), torch.Size((n, 14)), torch.float64
         self._term_b = self._term.view(torch.bool)
         self._trunc_b = self._trunc.view(torch.bool)
         self._succ_b = self._succ.view(torch.bool)
@@ -483,22 +484,26 @@ class MazeEnv:
         Returns (obs [N,29], reward, terminated, truncated, info{'success'}) as
         ``step`` does; with auto_reset, ``reset_states`` [N,29] (optional) are
         the caller's reset states for the envs that end (xy := init_xy)."""
-        torch = _torch()
         if self._loco_env_type != 'ant':
             raise ValueError('wrap_step() is for ant handles; point envs use step(action)')
+        # per-call host cost matters here (a 16k-env launch is ~5 us): one
+        # combined layout check, raw pointers, the cached output pointers
         q = qpos if qpos.is_contiguous() else qpos.contiguous()
         v = qvel if qvel.is_contiguous() else qvel.contiguous()
-        assert q.dtype == torch.float64 and v.dtype == torch.float64 and q.device == self.device
-        assert q.shape == (self.num_envs, 15) and v.shape == (self.num_envs, 14)
+        if (q.shape != self._ant_qshape or v.shape != self._ant_vshape or q.dtype != self._f64 or v.dtype != self._f64
+                or q.get_device() != self.device.index or v.get_device() != self.device.index):
+            raise ValueError(f'wrap_step: qpos/qvel must be float64 {tuple(self._ant_qshape)}/{tuple(self._ant_vshape)} '
+                             f'on {self.device}')
         rs = None
         if reset_states is not None:
+            torch = _torch()
             rs = torch.as_tensor(reset_states).to(self.device, torch.float64).contiguous()
             assert rs.shape == (self.num_envs, 29)
-        _lib.check(
-            self._L.ogbx_antmaze_step(self._h, _lib.ptr(q), _lib.ptr(v), *self._step_out[:5],
-                                      self._step_out[5], int(self.auto_reset), _lib.ptr(rs), self._stream()),
-            'wrap_step',
-        )
+            rs = rs.data_ptr()
+        st = self._L.ogbx_antmaze_step(self._h, q.data_ptr(), v.data_ptr(), *self._step_out, int(self.auto_reset), rs,
+                                       _lib.stream_of(self.device))
+        if st != 0:
+            _lib.check(st, 'wrap_step')
         info = {'success': self._succ_b}
         if self.auto_reset:
             info['final_observation'] = self._final_obs
