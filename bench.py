@@ -716,9 +716,16 @@ def bench_powder(args, world, rank, dev, level='easy'):
         data='synthetic (uniform valid Discrete actions per stage; Philox resets' + (' and rand fields)' if full else ')'),
         config=dict(workload=f'powderworld-{level}-v0 world_size=64', num_envs_per_gpu=n, auto_reset=True,
                     parallelism=f'env-shard x{world}'),
-        roofline=dict(bound='hbm', kernel=kern, achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic(kern, args.workload, n, world), kernel_ms=kern_ms,
-                      alg_bytes_per_launch=per_step * n),
+        # easy: HBM-bound; medium/hard: VALU issue-bound (one world per CU,
+        # its 16 waves keep the SIMDs issuing)
+        roofline=dict(bound='issue' if full else 'hbm', kernel=kern, achieved=achieved, peak=HBM_PEAK_GBS,
+                      unit='GB/s', frac=achieved / HBM_PEAK_GBS, traffic=_traffic(kern, args.workload, n, world),
+                      kernel_ms=kern_ms, alg_bytes_per_launch=per_step * n,
+                      alg_bytes_basis=(f'{per_step:.0f} B/env-step for the 10-byte cell state + goal ids (DESIGN 4.3)'
+                                       if full else
+                                       f'{per_step:.0f} B/env-step for the 1-byte cell state; supersedes SURVEY 8d\'s '
+                                       '55,979 B, which prices a 10-byte state whose extra channels the easy rules '
+                                       'never make non-zero (DESIGN 4.2)')),
         extra=extra,
     )
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
