@@ -74,15 +74,25 @@ def _max_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def _timed(fn, steps, world, dev):
+def _timed(fn, steps, world, dev, span=None):
+    """Wall time of `steps` calls between barrier + synchronize on both sides,
+    max over ranks.  span (a list): receives the device time of the same
+    region from a HIP event pair on the launch stream, in ms."""
     _barrier(world)
     torch.cuda.synchronize(dev)
+    if span is not None:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(torch.cuda.current_stream(dev))
     t0 = time.perf_counter()
     for i in range(steps):
         fn(i)
+    if span is not None:
+        b.record(torch.cuda.current_stream(dev))
     torch.cuda.synchronize(dev)
     _barrier(world)
     dt = time.perf_counter() - t0
+    if span is not None:
+        span.append(a.elapsed_time(b))
     return _max_over_ranks(dt, world, dev)
 
 
@@ -680,11 +690,14 @@ def bench_powder(args, world, rank, dev, level='easy'):
     for i in range(args.warmup):
         step(i)
     steps = args.steps - args.steps % 3 if args.steps >= 3 else args.steps
-    dt = _timed(step, steps, world, dev)
+    span = []
+    dt = _timed(step, steps, world, dev, span)
     value = n * steps * world / dt
-    # mean over whole 3-step action cycles (the forward runs on one step in
-    # three, so a per-launch median would pick a render-only step)
-    kern_ms = _per_launch_ms(step, min(steps, 201) - min(steps, 201) % 3 or 1, dev)
+    # device time per step of the timed region itself (one HIP event pair on
+    # the launch stream around it): the world's contents, and with them the
+    # forward's cost, drift over an episode, so a separate window would price
+    # different states; the mean also spans whole 3-step action cycles
+    kern_ms = span[0] / steps
     # algorithmic bytes per env-step: obs write H*W*6, world read H*W, world
     # write H*W on one step in three, action 4, reward 4, flags 3, ctrl 16.
     # medium/hard add momentum (1 B) + velocity (8 B) per cell read and
