@@ -683,12 +683,12 @@ ogbx_status ogbx_maze_create(const char* maze_type, int64_t n_envs, int32_t devi
   e->device = device;
   if (const char* v = std::getenv("OGBX_MAZE_LDS")) {  // diagnostic placement knob (A/B only)
     e->lds_pad = std::atoi(v);
-    hipFuncSetAttribute((const void*)maze_step_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
-    hipFuncSetAttribute((const void*)maze_step_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
-    hipFuncSetAttribute((const void*)maze_step_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
-    hipFuncSetAttribute((const void*)maze_step_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
-    hipFuncSetAttribute((const void*)point_physics_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
-    hipFuncSetAttribute((const void*)point_physics_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    (void)hipFuncSetAttribute((const void*)maze_step_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    (void)hipFuncSetAttribute((const void*)maze_step_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    (void)hipFuncSetAttribute((const void*)maze_step_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    (void)hipFuncSetAttribute((const void*)maze_step_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    (void)hipFuncSetAttribute((const void*)point_physics_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
+    (void)hipFuncSetAttribute((const void*)point_physics_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, e->lds_pad);
   }
   e->n = n_envs;
   MazeParams& P = e->P;

@@ -119,7 +119,11 @@ __device__ __forceinline__ uint32_t collide_roles(const PointModel& pm, const Ro
              b2 = cD & (fabs(dist2) * iw < 1.0);
   OGBX_WSTAT(10, b0 | b1 | b2);
   OGBX_WSTAT(11, cD);
+#ifndef OGBX_ABL_NOBAND
   if (__builtin_expect(__any(b0 | b1 | b2), 0)) {
+#else
+  if (false) {
+#endif
     if (b0) contact_gains(pm, dist0, &c.s0.w, &c.s0.kp);
     if (b1) contact_gains(pm, dist1, &c.s1.w, &c.s1.kp);
     if (b2) contact_gains(pm, dist2, &c.s2.w, &c.s2.kp);
@@ -300,7 +304,11 @@ __device__ __forceinline__ void solve_active_set(const PointModel& pm, const Con
   bool done = ((A2 ^ A) & valid) == 0u;
   OGBX_WSTAT(9, true);
   OGBX_WSTAT(13, !done);
+#ifndef OGBX_ABL_NODONE
   if (__builtin_expect(__any(!done), 0)) {
+#else
+  if (false) {
+#endif
 #pragma unroll 1
     for (int it = 0; it < 7 && !done; ++it) {
       OGBX_STAT(4);
@@ -333,7 +341,11 @@ __device__ __forceinline__ uint32_t stage_contacts(const PointModel& pm, const u
   uint32_t valid = collide_roles(pm, fr, x, y, c, &slow);
   *generic = false;
   OGBX_WSTAT(12, slow);
+#ifndef OGBX_ABL_NOSLOW
   if (__builtin_expect(__any(slow), 0)) {
+#else
+  if (false) {
+#endif
     *generic = true;
     role_tangents(c);
     if (slow) {
@@ -383,9 +395,11 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
     if (e != 0) {
       const double lim = 0.5 * pm.unit;
       const bool stale = !(fabs(qsx - fr.cx) <= lim) | !(fabs(qsy - fr.cy) <= lim);
+#ifndef OGBX_ABL_NOSTALE
       if (__builtin_expect(__any(stale), 0)) {
         if (stale) role_frame(pm, wall, H, W, qsx, qsy, fr);
       }
+#endif
       valid = stage_contacts(pm, wall, H, W, qsx, qsy, fr, c, &generic);
     }
     double fx, fy;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build _variants/libogbx_<name>.so: libogbx with locomaze.hip compiled under
+# extra flags (the other objects from build/obj, built by `make`).  Run here.
+# usage: scripts/build_maze_variant.sh <name> [-DFLAG ...]
+set -eu
+cd "$(dirname "$0")/.."
+name=$1; shift
+make -s -C ogbench_amd/csrc >/dev/null
+H=/opt/rocm/bin/hipcc
+F="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wno-unused-function -Wno-unused-variable -Wno-bitwise-instead-of-logical"
+$H $F "$@" -c ogbench_amd/csrc/locomaze.hip -o build/obj/locomaze_$name.o
+objs=$(ls build/obj/*.o | grep -v '/locomaze' | tr '\n' ' ')
+$H --offload-arch=gfx950 -shared -fPIC -o _variants/libogbx_$name.so $objs build/obj/locomaze_$name.o
+echo _variants/libogbx_$name.so
