@@ -8,7 +8,8 @@ name=$1; shift
 make -s -C ogbench_amd/csrc >/dev/null
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wno-unused-function -Wno-unused-variable -Wno-bitwise-instead-of-logical"
-$H $F "$@" -c ogbench_amd/csrc/locomaze.hip -o build/obj/locomaze_$name.o
+mkdir -p build/var
+$H $F "$@" -c ogbench_amd/csrc/locomaze.hip -o build/var/locomaze_$name.o
 objs=$(ls build/obj/*.o | grep -v '/locomaze' | tr '\n' ' ')
-$H --offload-arch=gfx950 -shared -fPIC -o _variants/libogbx_$name.so $objs build/obj/locomaze_$name.o
+$H --offload-arch=gfx950 -shared -fPIC -o _variants/libogbx_$name.so $objs build/var/locomaze_$name.o
 echo _variants/libogbx_$name.so

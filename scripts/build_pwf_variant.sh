@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build _variants/libogbx_pwf_<name>.so: libogbx with powder.hip compiled under
+# extra flags (the other objects from build/obj, built by `make`).  Run here.
+# usage: scripts/build_pwf_variant.sh <name> [-DOGBX_PWF_RULES=<mask> ...]
+set -eu
+cd "$(dirname "$0")/.."
+name=$1; shift
+make -s -C ogbench_amd/csrc >/dev/null
+H=/opt/rocm/bin/hipcc
+F="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -w"
+mkdir -p build/var
+$H $F "$@" -c ogbench_amd/csrc/powder.hip -o build/var/powder_$name.o
+objs=$(ls build/obj/*.o | grep -v '/powder' | tr '\n' ' ')
+$H --offload-arch=gfx950 -shared -fPIC -o _variants/libogbx_pwf_$name.so $objs build/var/powder_$name.o
+echo _variants/libogbx_pwf_$name.so
