@@ -804,7 +804,12 @@ struct FullWorld {
         ri = src[C + i];
         re = src[2 * C + i];
       } else {
+#ifdef OGBX_PWF_ABL_NORAND  // timing ablation: a cheap hash instead of Philox (changes the stream)
+        const uint32_t hh = ((uint32_t)i * 2654435761u) ^ (ep * 40503u) ^ (uint32_t)env ^ slot;
+        const u32x4 w = {hh, hh * 747796405u, hh * 2891336453u, hh};
+#else
         const u32x4 w = philox4x32_10({(uint32_t)i, (uint32_t)env, ep, slot}, k0 ^ (uint32_t)(env >> 32), k1);
+#endif
         rm = u01f_from(w.x);
         ri = u01f_from(w.y);
         re = u01f_from(w.z);
@@ -855,6 +860,9 @@ struct FullWorld {
 #ifdef OGBX_ASM_MARKS
     asm volatile("; ERR_BEGIN");
 #endif
+#ifdef OGBX_PWF_ABL_NOERR  // timing ablation
+    return 1 << 20;
+#endif
     fence_idx();
     int err = 0;
 #pragma unroll
@@ -886,6 +894,9 @@ struct FullWorld {
                                           bool rgb_only = false) const {
 #ifdef OGBX_ASM_MARKS
     asm volatile("; OBS_BEGIN");
+#endif
+#ifdef OGBX_PWF_ABL_NOOBS  // timing ablation
+    return;
 #endif
     fence_idx();
     const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
