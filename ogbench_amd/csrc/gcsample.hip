@@ -176,6 +176,30 @@ __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int6
   }
 }
 
+// The tile's Philox words, one call per lane: sample b of the tile, call q
+// (q < calls) -> wb[q][b].  A B = 1024 launch has two samples per workgroup,
+// so in-lane calls would run kCalls dependent-free chains on two lanes; spread
+// over 2 * kCalls lanes each lane runs one.  Same counters and keys as the
+// in-lane form, so the words are identical.
+#ifndef OGBX_GC_NOSPREAD
+constexpr bool kGcSpread = true;
+#else
+constexpr bool kGcSpread = false;
+#endif
+__device__ inline void tile_philox(uint4 (*wb)[kGcMaxTile], int calls, int n_here, int64_t base,
+                                   uint32_t call_lo, uint32_t call_hi, uint32_t k0, uint32_t k1) {
+  for (int t = threadIdx.x; t < calls * n_here; t += blockDim.x) {
+    const int b = t / calls, q = t - b * calls;
+    const uint64_t su = (uint64_t)(base + b);
+    const u32x4 w = philox4x32_10({(uint32_t)su, call_lo, (uint32_t)q, (uint32_t)(su >> 32) ^ call_hi}, k0, k1);
+    wb[q][b] = make_uint4(w.x, w.y, w.z, w.w);
+  }
+}
+__device__ inline u32x4 tile_word(const uint4 (*wb)[kGcMaxTile], int q, int b) {
+  const uint4 v = wb[q][b];
+  return u32x4{v.x, v.y, v.z, v.w};
+}
+
 template <bool kInj>
 __global__ void __launch_bounds__(256) gc_sample_kernel(
     ogbx_gc_buffer buf, ogbx_gc_config cfg, GcColumns cols, int32_t num_cols, int64_t total,
@@ -183,17 +207,29 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
     double v_log_q, double a_log_q, int64_t* idxs_out, int64_t* vgoal_out, int64_t* agoal_out,
     double* masks, double* rewards, ogbx_gc_draw_record rec, bool flat4) {
   __shared__ int64_t sel[4][kGcMaxTile];
+  __shared__ uint4 wb[(!kInj && kGcSpread) ? 5 : 1][kGcMaxTile];
   const int64_t base = (int64_t)blockIdx.x * tile;
   int n_here = (int)((total - base) < tile ? (total - base) : tile);
+  if (!kInj && kGcSpread) {
+    tile_philox(wb, 5, n_here, base, call_lo, call_hi, k0, k1);
+    __syncthreads();
+  }
   if (threadIdx.x < n_here) {
     const int64_t s = base + threadIdx.x;
     const uint64_t su = (uint64_t)s;
     const uint32_t c0 = (uint32_t)su, c3 = (uint32_t)(su >> 32) ^ call_hi;
-    const u32x4 w0 = philox4x32_10({c0, call_lo, 0u, c3}, k0, k1);
-    const u32x4 w1 = philox4x32_10({c0, call_lo, 1u, c3}, k0, k1);
-    const u32x4 w2 = philox4x32_10({c0, call_lo, 2u, c3}, k0, k1);
-    const u32x4 w3 = philox4x32_10({c0, call_lo, 3u, c3}, k0, k1);
-    const u32x4 w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
+    u32x4 w0, w1, w2, w3, w4;
+    if (!kInj && kGcSpread) {
+      const int b = (int)threadIdx.x;
+      w0 = tile_word(wb, 0, b), w1 = tile_word(wb, 1, b), w2 = tile_word(wb, 2, b), w3 = tile_word(wb, 3, b),
+      w4 = tile_word(wb, 4, b);
+    } else {
+      w0 = philox4x32_10({c0, call_lo, 0u, c3}, k0, k1);
+      w1 = philox4x32_10({c0, call_lo, 1u, c3}, k0, k1);
+      w2 = philox4x32_10({c0, call_lo, 2u, c3}, k0, k1);
+      w3 = philox4x32_10({c0, call_lo, 3u, c3}, k0, k1);
+      w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
+    }
     const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
     // sample index (datasets.py:65-70)
     int64_t idx = 0, pick = -1, final_idx;
@@ -268,17 +304,29 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     uint32_t call_hi, double v_log_q, double a_log_q, double l_log_q, ogbx_hgc_outputs o,
     ogbx_hgc_draw_record rec, bool flat4) {
   __shared__ int64_t sel[kHgcSel][kGcMaxTile];
+  __shared__ uint4 wb[(!kInj && kGcSpread) ? 7 : 1][kGcMaxTile];
   const int64_t base = (int64_t)blockIdx.x * tile;
   const int n_here = (int)((total - base) < tile ? (total - base) : tile);
+  if (!kInj && kGcSpread) {
+    tile_philox(wb, hc.has_low_value_goals ? 7 : 5, n_here, base, call_lo, call_hi, k0, k1);
+    __syncthreads();
+  }
   if (threadIdx.x < n_here) {
     const int64_t s = base + threadIdx.x;
     const uint64_t su = (uint64_t)s;
     const uint32_t c0 = (uint32_t)su, c3 = (uint32_t)(su >> 32) ^ call_hi;
-    const u32x4 w0 = philox4x32_10({c0, call_lo, 0u, c3}, k0, k1);
-    const u32x4 w1 = philox4x32_10({c0, call_lo, 1u, c3}, k0, k1);
-    const u32x4 w2 = philox4x32_10({c0, call_lo, 2u, c3}, k0, k1);
-    const u32x4 w3 = philox4x32_10({c0, call_lo, 3u, c3}, k0, k1);
-    const u32x4 w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
+    u32x4 w0, w1, w2, w3, w4;
+    if (!kInj && kGcSpread) {
+      const int b = (int)threadIdx.x;
+      w0 = tile_word(wb, 0, b), w1 = tile_word(wb, 1, b), w2 = tile_word(wb, 2, b), w3 = tile_word(wb, 3, b),
+      w4 = tile_word(wb, 4, b);
+    } else {
+      w0 = philox4x32_10({c0, call_lo, 0u, c3}, k0, k1);
+      w1 = philox4x32_10({c0, call_lo, 1u, c3}, k0, k1);
+      w2 = philox4x32_10({c0, call_lo, 2u, c3}, k0, k1);
+      w3 = philox4x32_10({c0, call_lo, 3u, c3}, k0, k1);
+      w4 = philox4x32_10({c0, call_lo, 4u, c3}, k0, k1);
+    }
     const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
     const ogbx_gc_draws& g = dr.gc;
     int64_t idx = 0, pick = -1, fin;
@@ -290,8 +338,13 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     u32x4 w5{}, w6{};
     int64_t l_rand = 0;
     if (hc.has_low_value_goals) {
-      w5 = philox4x32_10({c0, call_lo, 5u, c3}, k0, k1);
-      w6 = philox4x32_10({c0, call_lo, 6u, c3}, k0, k1);
+      if (!kInj && kGcSpread) {
+        w5 = tile_word(wb, 5, (int)threadIdx.x);
+        w6 = tile_word(wb, 6, (int)threadIdx.x);
+      } else {
+        w5 = philox4x32_10({c0, call_lo, 5u, c3}, k0, k1);
+        w6 = philox4x32_10({c0, call_lo, 6u, c3}, k0, k1);
+      }
       l.pick = (kInj && dr.l_pick) ? dr.l_pick[s] : (int64_t)bounded64(w5.x, w5.y, (uint64_t)npick);
     }
     index_loads(buf, kInj && g.idxs != nullptr, pick, &idx, &fin);

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build _variants/libogbx_<name>.so: libogbx with locomaze.hip compiled under
+# Build _variants/libogbx_<name>.so: libogbx with $SRC.hip (default locomaze) compiled under
 # extra flags (the other objects from build/obj, built by `make`).  Run here.
 # usage: scripts/build_maze_variant.sh <name> [-DFLAG ...]
 set -eu
@@ -9,7 +9,8 @@ make -s -C ogbench_amd/csrc >/dev/null
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wno-unused-function -Wno-unused-variable -Wno-bitwise-instead-of-logical"
 mkdir -p build/var
-$H $F "$@" -c ogbench_amd/csrc/locomaze.hip -o build/var/locomaze_$name.o
-objs=$(ls build/obj/*.o | grep -v '/locomaze' | tr '\n' ' ')
-$H --offload-arch=gfx950 -shared -fPIC -o _variants/libogbx_$name.so $objs build/var/locomaze_$name.o
+SRC=${SRC:-locomaze}
+$H $F "$@" -c ogbench_amd/csrc/$SRC.hip -o build/var/${SRC}_$name.o
+objs=$(ls build/obj/*.o | grep -v "/$SRC\.o" | tr '\n' ' ')
+$H --offload-arch=gfx950 -shared -fPIC -o _variants/libogbx_$name.so $objs build/var/${SRC}_$name.o
 echo _variants/libogbx_$name.so
