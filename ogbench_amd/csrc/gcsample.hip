@@ -503,8 +503,10 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
   ogbx_gc_draw_record rec{};
   if (record) rec = *record;
   const int64_t total = batch * num_batches;
-  // tile: enough workgroups to cover every CU (>= 512 when possible)
-  int64_t tile = total / 512;
+  // tile: one sample per workgroup up to 1024 samples (B = 1024: 1,024
+  // workgroups of 256 threads; measured against 2 and 4 samples per workgroup
+  // and 64- to 1024-thread workgroups), then up to 64 per workgroup
+  int64_t tile = total / 1024;
   if (tile < 1) tile = 1;
   if (tile > kGcMaxTile) tile = kGcMaxTile;
   const int64_t blocks = (total + tile - 1) / tile;
@@ -556,7 +558,7 @@ ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg
   ogbx_hgc_draw_record rec{};
   if (record) rec = *record;
   const int64_t total = batch * num_batches;
-  int64_t tile = total / 512;
+  int64_t tile = total / 1024;  // as ogbx_gc_sample
   if (tile < 1) tile = 1;
   if (tile > kGcMaxTile) tile = kGcMaxTile;
   const int64_t blocks = (total + tile - 1) / tile;
