@@ -39,6 +39,10 @@
 
 #include "point_physics.h"
 
+#ifndef OGBX_STAGE_UNROLL
+#define OGBX_STAGE_UNROLL 4
+#endif
+
 namespace ogbx {
 
 // Edge bits of slot s: 3s (n+t), 3s+1 (n-t), 3s+2 (n, weight 2w).
@@ -389,7 +393,7 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
   PieceWeights pw;
   piece_weights(act, pw);
   const int nstage = 4 * pm.nsub;
-#pragma unroll 4
+#pragma unroll OGBX_STAGE_UNROLL
   for (int e = 0; e < nstage; ++e) {
     const int st = e & 3;
     if (e != 0) {
