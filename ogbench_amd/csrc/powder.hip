@@ -40,6 +40,19 @@
 
 namespace ogbx {
 
+// Observation stores are streaming (123 MB per easy launch, written once and
+// far larger than L2): non-temporal 16-byte stores (`nt`), which do not
+// allocate in the cache (measured: easy 25.8 -> 23.5 us per launch).
+typedef unsigned int pw_u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void pw_nt_store16(uint4* d, const uint4& v) {
+#ifdef OGBX_PW_CACHED_OBS  // A/B: plain stores
+  *d = v;
+#else
+  pw_u32x4v x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<pw_u32x4v*>(d));
+#endif
+}
+
 constexpr int kPwMaxSeq = 256;
 constexpr int kPwMaxTasks = 8;
 constexpr uint32_t kIdMask = 31u, kGrav = 32u, kDidg = 64u;
@@ -344,7 +357,7 @@ struct Blk {
     const uint4* src = reinterpret_cast<const uint4*>(sh.ob);
     uint4* d = reinterpret_cast<uint4*>(dst);
 #pragma unroll
-    for (int q = t; q < G::OBS / 16; q += 256) d[q] = src[q];
+    for (int q = t; q < G::OBS / 16; q += 256) pw_nt_store16(&d[q], src[q]);
   }
 };
 
@@ -824,7 +837,7 @@ __global__ void __launch_bounds__(256) pwf_light_step_kernel(
   const uint4* src = reinterpret_cast<const uint4*>(st);
   uint4* d = reinterpret_cast<uint4*>(obs + (size_t)e * C * 6);
 #pragma unroll
-  for (int q = t; q < C * 6 / 16; q += 256) d[q] = src[q];
+  for (int q = t; q < C * 6 / 16; q += 256) pw_nt_store16(&d[q], src[q]);
 }
 
 // Free-standing PWSim.forward on worlds in the reference's (n, 9, H, W)

@@ -915,7 +915,7 @@ struct FullWorld {
     if (!rgb_only) {
       const uint4* src = reinterpret_cast<const uint4*>(s.ob);
       uint4* d = reinterpret_cast<uint4*>(dst);
-      for (int q = threadIdx.x; q < C * 6 / 16; q += NT) d[q] = src[q];
+      for (int q = threadIdx.x; q < C * 6 / 16; q += NT) pw_nt_store16(&d[q], src[q]);
     } else {
       const uint8_t* src = reinterpret_cast<const uint8_t*>(s.ob);
       for (int q = threadIdx.x; q < C * 3; q += NT) dst[q] = src[(q / 3) * 6 + q % 3];
