@@ -294,10 +294,12 @@ __device__ __forceinline__ void armijo_newton(const PointModel& pm, const Contac
 // On return *act_io is the mask of the converged build (pw its weights).
 // One iteration for every lane (straight line), more only while some lane's
 // mask still changes; after 8, the damped Newton finishes the lane.
-template <bool kRoles>
+// kBail: a lane still unconverged after the iterations sets *bail instead of
+// running the damped Newton (the caller redoes the step with the full loop).
+template <bool kRoles, bool kBail = false>
 __device__ __forceinline__ void solve_active_set(const PointModel& pm, const Contacts& c, uint32_t valid,
                                                  double vx, double vy, uint32_t* act_io, PieceWeights& pw,
-                                                 double* ux_out, double* uy_out) {
+                                                 double* ux_out, double* uy_out, bool* bail = nullptr) {
 #pragma clang fp contract(fast)
   const double mB = pm.mass * pm.B;
   const double mbvx = mB * vx, mbvy = mB * vy;
@@ -322,7 +324,9 @@ __device__ __forceinline__ void solve_active_set(const PointModel& pm, const Con
       A2 = edge_mask<kRoles>(c, ux, uy);
       done = ((A2 ^ A) & valid) == 0u;
     }
-    if (!done) {
+    if (kBail) {
+      *bail |= !done;
+    } else if (!done) {
       OGBX_STAT(5);
       armijo_newton<kRoles>(pm, c, valid, mbvx / pm.M, mbvy / pm.M, &ux, &uy);
       A = edge_mask<kRoles>(c, ux, uy) & valid;
@@ -364,25 +368,18 @@ __device__ __forceinline__ uint32_t stage_contacts(const PointModel& pm, const u
   return valid;
 }
 
-// One PointEnv physics step (same RK4 loop as point_physics.h point_step).
-__device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_t* wall, int H, int W,
-                                             double* px, double* py) {
-  double x = *px, y = *py;
-  Contacts c;
-  RoleFrame fr;
-  role_frame(pm, wall, H, W, x, y, fr);
-  bool generic;
-  uint32_t valid = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic);
-  const bool in_contact = valid != 0;
-  // Free lanes of a wave with a contact lane run the loop too (their result
-  // is discarded): the chain length, not the lane count, sets the wave's time,
-  // and gfx950 issues a dependent chain ~2x slower with <= 8 active lanes.
-  if (!__any(in_contact)) {
-    *px = x + 0.0;
-    *py = y + 0.0;
-    return 0;
-  }
-  const double x0 = x, y0 = y;
+// The 20-stage RK4 contact loop of one step from (x, y), whose first stage's
+// frame, contacts and collider choice the caller has computed.
+// kLean: the loop without the frame-refresh and generic-collider branches
+// (no lane's centre leaves its cell's inner part during the step: 0 % of the
+// bench's wave-stages) and without the damped-Newton safety net (never seen).  Instead of taking them it sets *bail on the lanes
+// that would have, and the caller redoes the step with the full loop; when
+// no lane bails, both loops execute the same arithmetic.
+template <bool kLean>
+__device__ __forceinline__ void contact_loop(const PointModel& pm, const uint16_t* wall, int H, int W, double& x,
+                                             double& y, RoleFrame fr, Contacts c, uint32_t valid, bool generic,
+                                             bool* bail) {
+  bool bl = false;
   const double h = pm.h;
   double vx = 0.0, vy = 0.0;
   double qsx = x, qsy = y, vsx = 0.0, vsy = 0.0;
@@ -399,18 +396,25 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
     if (e != 0) {
       const double lim = 0.5 * pm.unit;
       const bool stale = !(fabs(qsx - fr.cx) <= lim) | !(fabs(qsy - fr.cy) <= lim);
+      if (kLean) {
+        bool slow;
+        valid = collide_roles(pm, fr, qsx, qsy, c, &slow);
+        bl |= stale | slow;
+      } else {
 #ifndef OGBX_ABL_NOSTALE
-      if (__builtin_expect(__any(stale), 0)) {
-        if (stale) role_frame(pm, wall, H, W, qsx, qsy, fr);
-      }
+        if (__builtin_expect(__any(stale), 0)) {
+          if (stale) role_frame(pm, wall, H, W, qsx, qsy, fr);
+        }
 #endif
-      valid = stage_contacts(pm, wall, H, W, qsx, qsy, fr, c, &generic);
+        valid = stage_contacts(pm, wall, H, W, qsx, qsy, fr, c, &generic);
+      }
     }
     double fx, fy;
     {
 #pragma clang fp contract(fast)
       double ux, uy;
-      if (generic) solve_active_set<false>(pm, c, valid, vsx, vsy, &act, pw, &ux, &uy);
+      if (kLean) solve_active_set<true, true>(pm, c, valid, vsx, vsy, &act, pw, &ux, &uy, &bl);
+      else if (generic) solve_active_set<false>(pm, c, valid, vsx, vsy, &act, pw, &ux, &uy);
       else solve_active_set<true>(pm, c, valid, vsx, vsy, &act, pw, &ux, &uy);
       fx = ux - pm.B * vsx;
       fy = uy - pm.B * vsy;
@@ -441,6 +445,44 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
       }
     }
   }
+  *bail = bl;
+}
+
+// One PointEnv physics step (same RK4 loop as point_physics.h point_step).
+__device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_t* wall, int H, int W,
+                                             double* px, double* py) {
+  double x = *px, y = *py;
+  Contacts c;
+  RoleFrame fr;
+  role_frame(pm, wall, H, W, x, y, fr);
+  bool generic;
+  uint32_t valid = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic);
+  const bool in_contact = valid != 0;
+  // Free lanes of a wave with a contact lane run the loop too (their result
+  // is discarded): the chain length, not the lane count, sets the wave's time,
+  // and gfx950 issues a dependent chain ~2x slower with <= 8 active lanes.
+  if (!__any(in_contact)) {
+    *px = x + 0.0;
+    *py = y + 0.0;
+    return 0;
+  }
+  const double x0 = x, y0 = y;
+#ifndef OGBX_NO_LEAN_SPLIT
+  bool bail = true;
+  if (!__any(generic)) contact_loop<true>(pm, wall, H, W, x, y, fr, c, valid, false, &bail);
+  OGBX_WSTAT(14, bail);
+  if (__builtin_expect(__any(bail), 0)) {
+    // redo the step with the full loop from the same first stage
+    x = x0;
+    y = y0;
+    role_frame(pm, wall, H, W, x, y, fr);
+    valid = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic);
+    contact_loop<false>(pm, wall, H, W, x, y, fr, c, valid, generic, &bail);
+  }
+#else
+  bool bail;
+  contact_loop<false>(pm, wall, H, W, x, y, fr, c, valid, generic, &bail);
+#endif
   *px = in_contact ? x : x0 + 0.0;
   *py = in_contact ? y : y0 + 0.0;
   return in_contact ? 1 : 0;
