@@ -42,6 +42,10 @@
 // Stage-loop unroll (both the lean and the full loop of point_step_as): fully
 // unrolled, 20 stages.  Measured per launch at N = 65,536: 17.5 us; unroll 4
 // 18.0, 8 18.2, 2 18.9; lean loop 20 with the full loop 4: 18.3.
+// Active-set iterations of the lean loop before a lane bails to the full loop.
+#ifndef OGBX_LEAN_ITERS
+#define OGBX_LEAN_ITERS 7
+#endif
 #ifndef OGBX_AS_UNROLL
 #define OGBX_AS_UNROLL 20
 #endif
@@ -319,7 +323,7 @@ __device__ __forceinline__ void solve_active_set(const PointModel& pm, const Con
   if (false) {
 #endif
 #pragma unroll 1
-    for (int it = 0; it < 7 && !done; ++it) {
+    for (int it = 0; it < (kBail ? OGBX_LEAN_ITERS : 7) && !done; ++it) {
       OGBX_STAT(4);
       A = A2 & valid;
       piece_weights(A, pw);
