@@ -206,26 +206,6 @@ def bench_pointmaze(args, world, rank, dev):
                                  extra, env, kern_info)
     extra['eval_allgather'] = _eval_allgather(env, world, dev)
     env.reset(seed=0, options=dict(task_id=(torch.arange(base, base + n, dtype=torch.int32, device=dev) % 5) + 1))
-    # hipGraph replay of G steps (launch-bound inner loop captured once)
-    try:
-        G = 32
-        s = torch.cuda.Stream(dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            for i in range(3):
-                step(i)
-        torch.cuda.current_stream(dev).wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for i in range(G):
-                step(i)
-        for _ in range(3):
-            graph.replay()
-        reps = max(1, args.steps // G)
-        gdt = _timed(lambda i: graph.replay(), reps, world, dev)
-        extra['graph_replay_steps_per_s'] = total * G * reps / gdt
-    except Exception as e:  # pragma: no cover - reported, not fatal
-        extra['graph_replay_error'] = repr(e)[:200]
     # K fused steps per launch (K = 1 and K = 100)
     K = 100
     fused_actions = actions[:K].contiguous()
@@ -420,8 +400,8 @@ def bench_pointmaze_n1(args, world, rank, dev):
     """pointmaze-medium-navigate-v0 with ONE env (BASELINE configs[0]; SURVEY 8d
     row 1: plumbing).  A step = one Gymnasium-surface ``env.step(action)`` of
     the single env through the C-ABI (one launch), actions U[-1,1]^2 float32
-    from torch.Generator(seed=0) resident on the device, task round robin
-    1..5 per episode via same-step auto-reset (TimeLimit 1000).  The number is
+    from torch.Generator(seed=0) resident on the device, task 1 for every
+    episode (same-step auto-reset keeps the stored task; TimeLimit 1000).  The number is
     launch-latency bound by construction (one env); ``cpu_baseline`` is the
     oracle C restatement stepping the same single env on 1 core (the
     reference MuJoCo step cannot run here: MuJoCo is absent)."""
@@ -836,7 +816,7 @@ def bench_antmaze(args, world, rank, dev):
     R = 8
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
-    goal = info['goal'].clone()
+    goal = env.cur_goal_xy  # info['goal'] is the 29-d goal observation
     start = obs0[:, :2].clone()
     ring_q = torch.randn(R, n, 15, device=dev, dtype=torch.float64, generator=gen)
     ring_v = torch.randn(R, n, 14, device=dev, dtype=torch.float64, generator=gen)

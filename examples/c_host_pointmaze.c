@@ -131,7 +131,7 @@ static void run(int64_t n, int k, uint64_t seed, run_out* out) {
 }
 
 int main(int argc, char** argv) {
-  const int64_t n = argc > 1 ? atoll(argv[1]) : 4096;
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 65536;
   const int k = argc > 2 ? atoi(argv[2]) : 1100;
   if (ogbx_abi_version() != OGBX_ABI_VERSION) {
     fprintf(stderr, "ABI mismatch: header %d, library %d\n", OGBX_ABI_VERSION, ogbx_abi_version());

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define OGBX_ABI_VERSION 2
+#define OGBX_ABI_VERSION 3
 
 typedef enum {
   OGBX_OK = 0,
@@ -75,7 +75,13 @@ typedef struct {
                                 counted by the GLOBAL env index env_base + i, so
                                 G ranks holding envs [r*N/G, (r+1)*N/G) with one
                                 shared seed reproduce the single-GPU run of N
-                                envs bit for bit.  0 = unsharded. */
+                                envs bit for bit.  0 = unsharded.
+                                Shard boundaries must be multiples of 64 envs:
+                                the contact solver's wave-uniform path choices
+                                depend on which 64 envs share a wavefront, so a
+                                boundary inside a wave changes results at the
+                                rounding level (ogbench_amd.sharding.shard
+                                enforces this). */
 } ogbx_maze_opts;
 
 /* Create a batch of `n_envs` maze envs on `device`.
@@ -165,12 +171,19 @@ ogbx_status ogbx_antmaze_state(ogbx_maze_t env, double** body_qpos, double** bod
  * uniform(-0.1, 0.1)^15, qvel = 0.1 * normal^14, then set_xy(init_xy).
  *   body_draws  device f64[N,29] = the 15 uniform(-0.1,0.1) and 14 standard
  *               normal draws in reset_model order, or NULL = Philox.
- *   obs         device f64[N,29] out; goal device f64[N,2] out (the goal xy:
- *               info['goal'] as the oracle representation -- the full goal
- *               observation needs physics, maze.py:407-418). */
+ *   goal_states device f64[N,29] (qpos, qvel) = the body state the caller's
+ *               physics reached after the reference's goal reset and its 5
+ *               random-action steps (maze.py:408-413), or NULL: the goal
+ *               reset's reset_model state (Philox) stands in, unstepped.
+ *   obs         device f64[N,29] out; goal device f64[N,2] out = the goal xy
+ *               (cur_goal_xy; info['goal'] under use_oracle_rep, maze.py:482-484).
+ *   goal_ob     device f64[N,29] out (nullable) = info['goal'], the goal
+ *               observation: goal_states with qpos[:2] := goal xy
+ *               (set_xy + get_ob, maze.py:416-418, ant.py:97-122). */
 ogbx_status ogbx_antmaze_reset(ogbx_maze_t env, const int32_t* task_id, const double* task_xy,
                                const uint8_t* mask, const double* noise, const double* body_draws,
-                               double* obs, double* goal, uint64_t seed, void* stream);
+                               const double* goal_states, double* obs, double* goal, double* goal_ob,
+                               uint64_t seed, void* stream);
 
 /* MazeEnv.step + TimeLimit for an ant handle, given the post-physics state
  * qpos_post f64[N,15] / qvel_post f64[N,14] -- either the handle's own state

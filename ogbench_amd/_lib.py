@@ -81,7 +81,8 @@ _SIGNATURES = {
     'ogbx_antmaze_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p)]),
     'ogbx_antmaze_reset': (
         c_int32,
-        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p],
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_uint64, c_void_p],
     ),
     'ogbx_antmaze_step': (
         c_int32,
@@ -160,9 +161,15 @@ def lib():
                 f'There is no CPU fallback.'
             )
         handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        # Every entry point include/ogbx.h declares must be exported, whichever
+        # library is loaded (the in-tree build or an OGBX_LIB override): a stale
+        # or partial library fails here, not at the first call of a missing symbol.
+        missing = [n for n in declared_symbols() if not hasattr(handle, n)]
+        missing += [n for n in _SIGNATURES if not hasattr(handle, n)]
+        if missing:
+            raise RuntimeError(f'{LIB_PATH} lacks entry points declared in {HEADER_PATH}: '
+                               f'{", ".join(sorted(set(missing)))}; rebuild it (make -C ogbench_amd/csrc)')
         for name, (res, args) in _SIGNATURES.items():
-            if not hasattr(handle, name):
-                continue
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args

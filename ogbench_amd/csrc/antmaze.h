@@ -19,9 +19,13 @@
 //   optional same-step auto-reset (below).
 // Reset (maze.py:373-431 with AntEnv.reset_model, ant.py:103-111): the
 // returned ob is the second reset's state, qpos = init_qpos + U(-0.1, 0.1)^15,
-// qvel = 0.1 N(0,1)^14, then set_xy(init_xy) -- no physics.  (The first reset
-// + 5 random steps only feed info['goal'] as a full observation, which needs
-// the physics engine; the wrapper returns the goal xy, i.e. the oracle rep.)
+// qvel = 0.1 N(0,1)^14, then set_xy(init_xy) -- no physics.  info['goal'] is
+// the goal OBSERVATION (maze.py:407-418): the body state after the first reset
+// and 5 random-action physics steps, with set_xy(goal_xy).  Those steps are the
+// caller's physics, so the caller hands that state in (goal_states [N,29]) and
+// the kernel writes it with qpos[:2] := goal_xy; without it, the first
+// reset_model state (Philox, its own counter slots) stands in for the stepped
+// one.  The oracle representation (use_oracle_rep) is the goal xy.
 // The body draws come from Philox (tag kTagAntBody) or from the caller:
 // injected draws [N,29] (parity) or whole reset states [N,29] produced by the
 // caller's own physics reset (auto-reset), whose xy is then set to init_xy.
@@ -39,8 +43,11 @@ __device__ __forceinline__ double ant_init_qpos(int c) {
 
 // The c-th body draw of env gi's episode ep: c < 15 -> uniform(-0.1, 0.1),
 // c >= 15 -> standard normal (Box-Muller on two Philox uniforms).
-__device__ inline double ant_body_draw(uint64_t gi, uint32_t ep, int c, uint32_t k0, uint32_t k1) {
-  const u32x4 w = philox4x32_10({(uint32_t)gi, ep, 0x300u + (uint32_t)c, (uint32_t)(gi >> 32)}, k0 ^ kTagAntBody, k1);
+// slot: 0x300 for the reset_model that sets the returned ob, 0x340 for the
+// first (goal) reset_model of MazeEnv.reset.
+__device__ inline double ant_body_draw(uint64_t gi, uint32_t ep, int c, uint32_t k0, uint32_t k1,
+                                      uint32_t slot = 0x300u) {
+  const u32x4 w = philox4x32_10({(uint32_t)gi, ep, slot + (uint32_t)c, (uint32_t)(gi >> 32)}, k0 ^ kTagAntBody, k1);
   const double u0 = u01_from(w.x, w.y), u1 = u01_from(w.z, w.w);
   if (c < kAntNq) return -0.1 + 0.2 * u0;
   const double r = sqrt(-2.0 * log1p(-u0));  // 1 - u0 in (0, 1]
@@ -68,7 +75,8 @@ __global__ void __launch_bounds__(256) ant_reset_kernel(const MazeParams* __rest
                                                         double* __restrict__ bq, double* __restrict__ bv, int64_t n,
                                                         const int32_t* task_id, const double* task_xy,
                                                         const uint8_t* mask, const double* noise,
-                                                        const double* body_draws, double* obs, double* goal_out,
+                                                        const double* body_draws, const double* goal_states,
+                                                        double* obs, double* goal_out, double* goal_ob,
                                                         uint32_t k0, uint32_t k1) {
   const MazeParams& P = *Pp;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -108,6 +116,18 @@ __global__ void __launch_bounds__(256) ant_reset_kernel(const MazeParams* __rest
   S.episode[i] = ep;
   goal_out[2 * i] = gx;
   goal_out[2 * i + 1] = gy;
+  if (goal_ob != nullptr) {
+    // get_ob() after the goal reset's random steps and set_xy(goal_xy)
+    double* g = goal_ob + (int64_t)kAntOb * i;
+    const double* gs = goal_states ? goal_states + (int64_t)kAntOb * i : nullptr;
+    for (int c = 0; c < kAntOb; ++c) {
+      double val;
+      if (gs) val = gs[c];
+      else if (c < kAntNq) val = ant_init_qpos(c) + ant_body_draw(gi, ep, c, k0, k1, 0x340u);
+      else val = 0.0 + 0.1 * ant_body_draw(gi, ep, c, k0, k1, 0x340u);
+      g[c] = c == 0 ? gx : (c == 1 ? gy : val);
+    }
+  }
 }
 
 // Row kinds decided in phase A of ant_step_kernel.

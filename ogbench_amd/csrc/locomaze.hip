@@ -912,8 +912,8 @@ ogbx_status ogbx_antmaze_state(ogbx_maze_t e, double** body_qpos, double** body_
 }
 
 ogbx_status ogbx_antmaze_reset(ogbx_maze_t e, const int32_t* task_id, const double* task_xy, const uint8_t* mask,
-                               const double* noise, const double* body_draws, double* obs, double* goal,
-                               uint64_t seed, void* stream) {
+                               const double* noise, const double* body_draws, const double* goal_states,
+                               double* obs, double* goal, double* goal_ob, uint64_t seed, void* stream) {
   OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
   OGBX_CHECK(e->P.loco_type == 1, OGBX_EINVAL, "ogbx_antmaze_reset: not an ant handle");
   OGBX_CHECK(obs != nullptr && goal != nullptr, OGBX_EINVAL, "ogbx_antmaze_reset: null output");
@@ -922,7 +922,8 @@ ogbx_status ogbx_antmaze_reset(ogbx_maze_t e, const int32_t* task_id, const doub
   uint32_t k0, k1;
   seed_key(seed, kTagMazeReset, &k0, &k1);
   hipLaunchKernelGGL(ant_reset_kernel, dim3(grid_for(e->n, 256)), dim3(256), 0, (hipStream_t)stream, e->Pd, e->S,
-                     e->body_qpos, e->body_qvel, e->n, task_id, task_xy, mask, noise, body_draws, obs, goal, k0, k1);
+                     e->body_qpos, e->body_qvel, e->n, task_id, task_xy, mask, noise, body_draws, goal_states, obs,
+                     goal, goal_ob, k0, k1);
   OGBX_LAUNCHED("ant_reset_kernel");
   e->was_reset = true;
   return OGBX_OK;
@@ -960,15 +961,19 @@ ogbx_status ogbx_maze_rollout_until_done(ogbx_maze_t e, const void* action, int3
              "ogbx_maze_rollout_until_done: null argument");
   OGBX_CHECK(k_steps >= 1, OGBX_EINVAL, "k_steps must be >= 1");
   OGBX_HIP(hipSetDevice(e->device));
+  // Same Philox key as ogbx_maze_step: the teleport out-portal draw of a rollout row
+  // must equal that of the single step it stands for.
+  uint32_t k0, k1;
+  seed_key(e->seed, kTagMazeReset, &k0, &k1);
   const int epw = e->epw;
   dim3 grid(grid_for(e->n * (64 / epw), kStepBlock)), block(kStepBlock);
   if (action_is_f64)
     hipLaunchKernelGGL((maze_step_kernel<true, true>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
-                       e->n, action, k_steps, obs, reward, terminated, truncated, success, nullptr, 0, 0u, 0u,
+                       e->n, action, k_steps, obs, reward, terminated, truncated, success, nullptr, 0, k0, k1,
                        epw, steps_taken);
   else
     hipLaunchKernelGGL((maze_step_kernel<false, true>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
-                       e->n, action, k_steps, obs, reward, terminated, truncated, success, nullptr, 0, 0u, 0u,
+                       e->n, action, k_steps, obs, reward, terminated, truncated, success, nullptr, 0, k0, k1,
                        epw, steps_taken);
   OGBX_LAUNCHED("maze_step_kernel");
   return OGBX_OK;

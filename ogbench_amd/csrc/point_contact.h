@@ -43,9 +43,15 @@
 // unrolled, 20 stages.  Measured per launch at N = 65,536: 17.5 us; unroll 4
 // 18.0, 8 18.2, 2 18.9; lean loop 20 with the full loop 4: 18.3.
 // Active-set iterations of the lean loop before a lane bails to the full loop.
+// Full-loop active-set iterations before the damped-Newton safety net.  The
+// lean loop must not iterate longer: a lane it accepts after more iterations
+// would be one the full loop hands to armijo_newton, and its result would
+// depend on which loop its wave ran.
+#define OGBX_FULL_ITERS 7
 #ifndef OGBX_LEAN_ITERS
-#define OGBX_LEAN_ITERS 7
+#define OGBX_LEAN_ITERS OGBX_FULL_ITERS
 #endif
+static_assert(OGBX_LEAN_ITERS <= OGBX_FULL_ITERS, "lean loop may not iterate longer than the full loop");
 #ifndef OGBX_AS_UNROLL
 #define OGBX_AS_UNROLL 20
 #endif
@@ -323,7 +329,7 @@ __device__ __forceinline__ void solve_active_set(const PointModel& pm, const Con
   if (false) {
 #endif
 #pragma unroll 1
-    for (int it = 0; it < (kBail ? OGBX_LEAN_ITERS : 7) && !done; ++it) {
+    for (int it = 0; it < (kBail ? OGBX_LEAN_ITERS : OGBX_FULL_ITERS) && !done; ++it) {
       OGBX_STAT(4);
       A = A2 & valid;
       piece_weights(A, pw);

@@ -89,7 +89,10 @@ class MazeEnv:
     ):
         """env_base: global index of env 0 of this batch.  Every Philox stream
         is counted by the global env index, so G shards [r*N/G, (r+1)*N/G) with
-        the same seed reproduce one batch of N envs bit for bit."""
+        the same seed reproduce one batch of N envs bit for bit.
+        Shard boundaries must be multiples of 64 envs (the contact solver's
+        wave-uniform choices depend on which envs share a wavefront); use
+        ogbench_amd.sharding.shard."""
         if loco_env_type not in LOCO_TYPES:
             raise ValueError(f'Unknown locomotion environment type: {loco_env_type}')
         if maze_type not in MAZE_TYPES:
@@ -166,6 +169,8 @@ class MazeEnv:
         self._ob_dim = 2 if loco_env_type == 'point' else ob_dim
         self._obs = torch.zeros(n, self._ob_dim, dtype=torch.float64, **kw)
         self._goal = torch.zeros(n, 2, dtype=torch.float64, **kw)
+        # ant: info['goal'] is the 29-d goal observation (maze.py:407-418)
+        self._goal_ob = torch.zeros(n, ob_dim, dtype=torch.float64, **kw) if loco_env_type == 'ant' else None
         self._final_obs = torch.zeros(n, self._ob_dim, dtype=torch.float64, **kw)
         self._reward = torch.zeros(n, dtype=torch.float32, **kw)
         self._term = torch.zeros(n, dtype=torch.uint8, **kw)
@@ -361,8 +366,14 @@ class MazeEnv:
         init_ij/goal_ij, or an [N,4] xy tensor), ``noise`` ([N,4] injected
         uniform(-1,1) draws; test hook), ``render_goal`` (unsupported); ant
         handles also take ``body_draws`` ([N,29] injected AntEnv.reset_model
-        draws: 15 uniform(-0.1,0.1), 14 standard normal).
-        Returns (obs [N,2] f64 (point) | [N,29] f64 (ant), {'goal': [N,2] f64}).
+        draws: 15 uniform(-0.1,0.1), 14 standard normal) and ``goal_states``
+        ([N,29] f64, the body state (qpos, qvel) the caller's physics reached
+        after the goal reset and its 5 random-action steps, maze.py:408-413).
+        Returns (obs, {'goal': goal}): point obs/goal [N,2] f64; ant obs [N,29]
+        and goal = the goal observation [N,29] (goal_states with qpos[:2] :=
+        goal_xy, maze.py:416-418; without goal_states the goal reset's
+        unstepped reset_model state stands in), or the goal xy [N,2] under
+        use_oracle_rep (maze.py:418,482-484).
         """
         if self._loco_env_type == 'humanoid':
             raise NotImplementedError('humanoid dynamics and its observation layout are out of scope')
@@ -402,14 +413,19 @@ class MazeEnv:
             if bd is not None:
                 bd = torch.as_tensor(bd).to(self.device, torch.float64).contiguous()
                 assert bd.shape == (self.num_envs, 29)
+            gs = options.get('goal_states')
+            if gs is not None:
+                gs = torch.as_tensor(gs).to(self.device, torch.float64).contiguous()
+                assert gs.shape == (self.num_envs, 29), 'goal_states must be [num_envs, 29] (qpos, qvel)'
+            gob = None if self._use_oracle_rep else self._goal_ob
             _lib.check(
                 self._L.ogbx_antmaze_reset(self._h, _lib.ptr(task_t), _lib.ptr(task_xy), _lib.ptr(m),
-                                           _lib.ptr(noise), _lib.ptr(bd), _lib.ptr(self._obs), _lib.ptr(self._goal),
-                                           self._seed, self._stream()),
+                                           _lib.ptr(noise), _lib.ptr(bd), _lib.ptr(gs), _lib.ptr(self._obs),
+                                           _lib.ptr(self._goal), _lib.ptr(gob), self._seed, self._stream()),
                 'reset',
             )
             self._has_reset = True
-            return self._obs, {'goal': self._goal}
+            return self._obs, {'goal': self._goal if self._use_oracle_rep else self._goal_ob}
         _lib.check(
             self._L.ogbx_maze_reset(
                 self._h,

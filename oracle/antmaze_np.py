@@ -55,6 +55,15 @@ def reset_obs(task, noise, body_draws, tasks=LARGE_TASKS):
     return ob, goal
 
 
+def goal_obs(goal, goal_states):
+    """info['goal'] of MazeEnv.reset (maze.py:407-418): the body state after
+    the goal reset's random physics steps (given, [N,29]) with set_xy(goal_xy),
+    as get_ob() concatenates it (ant.py:97-122)."""
+    g = np.array(goal_states, np.float64, copy=True)
+    g[:, :2] = goal
+    return g
+
+
 class Batch:
     """State of N antmaze envs between wrapper steps."""
 

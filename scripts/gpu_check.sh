@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-2 GPU check: gpu tests, smoke, default bench, pointmaze-medium N=1 bench,
+# Round GPU check: gpu tests, smoke, default bench, pointmaze-medium N=1 bench,
 # 2-rank gloo rehearsal of the strong-scaling pointmaze bench.  Every GPU step
 # has its own time limit; the script stops at the first crash / timeout.
 set -u

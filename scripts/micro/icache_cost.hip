@@ -4,7 +4,7 @@
 // cold after the dispatch's cache invalidation) or as a 64-instruction loop
 // body run K/64 times (warm after the first pass).  Difference = fetch cost.
 // One wave per SIMD (256 x 256 threads) and the 8-GPU strong share (32 x 256).
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/icache_cost.hip -o _variants/icache_cost
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/icache_cost.hip -o _ab/icache_cost
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -1,7 +1,7 @@
 // Microbenchmark (not shipped): does the cost of a dependent fp64 chain depend
 // on how many lanes of the wave are active?  256 workgroups x 256 threads (one
 // wave per SIMD); in every wave lanes < k run the chain, the rest skip it.
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/lane_count.hip -o _variants/lane_count
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/lane_count.hip -o _ab/lane_count
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #pragma clang diagnostic ignored "-Wunused-result"

@@ -2,7 +2,7 @@
 // property of the wave or of the SIMD?  256 workgroups x 512 threads (two
 // waves per SIMD); waves 0-3 run a dependent fp64 FMA chain on k0 lanes,
 // waves 4-7 on k1 lanes.
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/lane_mix.hip -o _variants/lane_mix
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/lane_mix.hip -o _ab/lane_mix
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #pragma clang diagnostic ignored "-Wunused-result"

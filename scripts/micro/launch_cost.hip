@@ -3,7 +3,7 @@
 // dependent read of a parameter block, with an LDS staging barrier, with a
 // large VGPR allocation, and with byte flag stores.  Back-to-back launches
 // (total / count) and event-pair medians.
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/launch_cost.hip -o _variants/launch_cost
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/launch_cost.hip -o _ab/launch_cost
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -1,6 +1,6 @@
 // Microbenchmark (not shipped): relative error of v_rcp_f64 alone and with one
 // or two Newton-Raphson refinements against the IEEE quotient 1.0 / d.
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/rcp_err.hip -o _variants/rcp_err
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/rcp_err.hip -o _ab/rcp_err
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>

@@ -1,6 +1,6 @@
 // Microbenchmark (not shipped): per-wave cycles of dependent / independent
 // fp64 VALU chains on gfx950, one or two waves per SIMD.
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/valu_lat.hip -o _variants/valu_lat
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/valu_lat.hip -o _ab/valu_lat
 #include <hip/hip_runtime.h>
 #include <cstdio>
 

@@ -15,9 +15,19 @@ reference.  gymnasium's TimeLimit is restated (elapsed += 1; truncated when
 elapsed >= max_episode_steps).  Every draw is recorded: np.random.uniform of
 add_noise and the env's np_random draws of reset_model.  Only inputs and
 outputs are saved.
+
+info['goal'] is the reference's goal observation (maze.py:407-418): the stub's
+5 random steps load the last of five given states, so `goal_states` (that
+state) is the input and `reset_goal_ob` (info['goal'] itself) the output.
+
+Provenance: the npz records the sha256 of every method source extracted from
+the reference (`src_sha256`, one line per method) and the reference's git HEAD
+when readable, so a reviewer can audit what was executed.  Run it only in a
+sandbox (this container): it executes reference code.
 """
 
 import ast
+import hashlib
 import os
 import textwrap
 
@@ -25,6 +35,17 @@ import numpy as np
 
 REF = os.environ.get('OGBENCH_REF', '/root/reference')
 OUT = os.path.dirname(os.path.abspath(__file__))
+_PROVENANCE = {}
+
+
+def _ref_head():
+    try:
+        head = open(os.path.join(REF, '.git', 'HEAD')).read().strip()
+        if head.startswith('ref: '):
+            head = open(os.path.join(REF, '.git', head[5:])).read().strip()
+        return head
+    except OSError:
+        return 'unknown'
 
 
 def _methods(path, cls_name, names, factory=None):
@@ -37,7 +58,9 @@ def _methods(path, cls_name, names, factory=None):
     out = []
     for node in cls.body:
         if isinstance(node, ast.FunctionDef) and node.name in names:
-            out.append(textwrap.dedent(ast.get_source_segment(src, node)))
+            seg = textwrap.dedent(ast.get_source_segment(src, node))
+            _PROVENANCE[f'{path}:{cls_name}.{node.name}'] = hashlib.sha256(seg.encode()).hexdigest()
+            out.append(seg)
     assert len(out) == len(names), (cls_name, names)
     return out
 
@@ -154,6 +177,8 @@ def antmaze_golden(rng, n=24, T=40, max_steps=30):
         body = np.zeros((n, 29))
         robs = np.zeros((n, 29))
         rgoal = np.zeros((n, 2))
+        gstates = np.zeros((n, 29))
+        gob = np.zeros((n, 29))
         qpost = np.zeros((T, n, 15))
         vpost = np.zeros((T, n, 14))
         obs = np.zeros((T, n, 29))
@@ -163,8 +188,8 @@ def antmaze_golden(rng, n=24, T=40, max_steps=30):
         succ = np.zeros((T, n), np.uint8)
         for i in range(n):
             env_rng = _Rec(np.random.RandomState(int(rng.randint(1 << 30))))
-            reset_feed = iter([(rng.normal(size=15), rng.normal(size=14)) for _ in range(5)])
-            env = make_env(cls, 'large', reset_feed, env_rng, timing)
+            feed = [(rng.normal(size=15), rng.normal(size=14)) for _ in range(5)]
+            env = make_env(cls, 'large', iter(feed), env_rng, timing)
             rec.log.clear()
             env_rng.log.clear()
             ob, info = env.reset(options=dict(task_id=int(tasks[i])))
@@ -176,6 +201,8 @@ def antmaze_golden(rng, n=24, T=40, max_steps=30):
             body[i, 15:] = draws[1][1]
             robs[i] = ob
             rgoal[i] = env.cur_goal_xy
+            gstates[i] = np.concatenate(feed[-1])  # state after the 5 random steps
+            gob[i] = info['goal']  # the reference's goal observation
             # post-physics states: half the envs walk onto the goal (success ->
             # terminated), the rest wander; every other coordinate random
             xy0 = np.array(env.get_xy())
@@ -202,9 +229,12 @@ def antmaze_golden(rng, n=24, T=40, max_steps=30):
                 succ[t, i] = inf['success']
         p = f'{timing}_'
         out.update({p + 'task': tasks, p + 'noise': noise, p + 'body_draws': body, p + 'reset_obs': robs,
-                    p + 'reset_goal': rgoal, p + 'qpos_post': qpost, p + 'qvel_post': vpost, p + 'obs': obs,
+                    p + 'reset_goal': rgoal, p + 'goal_states': gstates, p + 'reset_goal_ob': gob,
+                    p + 'qpos_post': qpost, p + 'qvel_post': vpost, p + 'obs': obs,
                     p + 'reward': rew, p + 'terminated': term, p + 'truncated': trunc, p + 'success': succ})
     out['max_episode_steps'] = np.array(max_steps, np.int32)
+    out['src_sha256'] = np.array(sorted(f'{k} {v}' for k, v in _PROVENANCE.items()))
+    out['ref_head'] = np.array(_ref_head())
     return out
 
 

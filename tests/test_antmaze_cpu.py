@@ -23,6 +23,7 @@ def test_oracle_matches_reference_fixture(timing):
     ob0, goal = am.reset_obs(g['task'], g['noise'], g['body_draws'])
     assert np.array_equal(ob0, g['reset_obs'])
     assert np.array_equal(goal, g['reset_goal'])
+    assert np.array_equal(am.goal_obs(goal, g['goal_states']), g['reset_goal_ob'])
     b = am.Batch(g['task'], g['noise'], g['body_draws'], max_steps=int(d['max_episode_steps']), timing=timing)
     for k in range(g['obs'].shape[0]):
         obs, rew, term, trunc, succ = b.step(g['qpos_post'][k], g['qvel_post'][k])

@@ -39,10 +39,14 @@ def test_wrapper_matches_reference(gpu, golden, timing, in_place):
     n = g['task'].shape[0]
     env = _env(gpu, n, timing, max_episode_steps=int(golden['max_episode_steps']))
     obs, info = env.reset(seed=0, options=dict(task_id=torch.tensor(g['task']), noise=torch.tensor(g['noise']),
-                                               body_draws=torch.tensor(g['body_draws'])))
+                                               body_draws=torch.tensor(g['body_draws']),
+                                               goal_states=torch.tensor(g['goal_states'])))
     assert obs.shape == (n, 29)
     assert np.array_equal(obs.cpu().numpy(), g['reset_obs'])
-    assert np.array_equal(info['goal'].cpu().numpy(), g['reset_goal'])
+    # info['goal'] is the reference's 29-d goal observation (maze.py:407-418)
+    assert info['goal'].shape == (n, 29)
+    assert np.array_equal(info['goal'].cpu().numpy(), g['reset_goal_ob'])
+    assert np.array_equal(env.cur_goal_xy.cpu().numpy(), g['reset_goal'])
     bq, bv = env.body_state()
     for t in range(g['obs'].shape[0]):
         q = torch.tensor(g['qpos_post'][t], device=gpu)
@@ -62,6 +66,33 @@ def test_wrapper_matches_reference(gpu, golden, timing, in_place):
         assert np.array_equal(bv.cpu().numpy(), g['qvel_post'][t])
         assert np.array_equal(env.get_xy().cpu().numpy(), g['qpos_post'][t][:, :2])
     assert g['terminated'].sum() > 50 and g['truncated'].sum() > 50
+
+
+def test_goal_observation_oracle_rep_and_standin(gpu, golden):
+    """use_oracle_rep: info['goal'] = the goal xy (get_oracle_rep, maze.py:482-484).
+    Without goal_states: a 29-d goal observation whose xy is the goal and whose
+    other coordinates are an unstepped reset_model state (qpos0 + U(-0.1, 0.1),
+    0.1 N(0, 1)) from Philox, distinct from the returned ob's draws."""
+    g = {k[5:]: v for k, v in golden.items() if k.startswith('post_')}
+    n = g['task'].shape[0]
+    opts = dict(task_id=torch.tensor(g['task']), noise=torch.tensor(g['noise']),
+                body_draws=torch.tensor(g['body_draws']), goal_states=torch.tensor(g['goal_states']))
+    env = _env(gpu, n, 'post', use_oracle_rep=True)
+    obs, info = env.reset(seed=0, options=opts)
+    assert info['goal'].shape == (n, 2)
+    assert np.array_equal(info['goal'].cpu().numpy(), g['reset_goal'])
+    assert np.array_equal(obs.cpu().numpy(), g['reset_obs'])
+    m = 1 << 14
+    env = _env(gpu, m, 'post')
+    obs, info = env.reset(seed=3, options=dict(task_id=2))
+    go, ob = info['goal'].cpu().numpy(), obs.cpu().numpy()
+    assert go.shape == (m, 29)
+    assert np.array_equal(go[:, :2], env.cur_goal_xy.cpu().numpy())
+    q0 = np.array([0, 0, 0.75, 1, 0, 0, 0] + [0] * 8, np.float64)
+    assert np.abs(go[:, 2:15] - q0[2:]).max() <= 0.1
+    z = go[:, 15:] / 0.1
+    assert abs(z.mean()) < 1e-2 and abs(z.std() - 1.0) < 1e-2
+    assert not np.any(go[:, 2:] == ob[:, 2:])  # independent of the ob's draws
 
 
 def test_auto_reset_with_caller_reset_states(gpu):

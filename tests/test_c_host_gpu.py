@@ -16,7 +16,7 @@ EXE = os.path.join(ROOT, 'examples', 'c_host_pointmaze')
 
 def test_c_host_drives_the_c_abi():
     assert os.path.exists(EXE), 'examples/c_host_pointmaze not built (run __graft_entry__.build())'
-    out = subprocess.run([EXE, '4096', '1100'], capture_output=True, text=True, timeout=180)
+    out = subprocess.run([EXE, '65536', '1100'], capture_output=True, text=True, timeout=180)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.strip().endswith('OK'), out.stdout
-    assert 'episodes=4096' in out.stdout
+    assert 'episodes=65536' in out.stdout

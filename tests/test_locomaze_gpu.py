@@ -330,3 +330,45 @@ def test_medium_single_env_timelimit_episode(gpu, task):
         assert bool(tr[0]) == (t == 999) == bool(ref['truncated'][0, 0]), t
         assert float(r[0]) == float(ref['reward'][0, 0])
     assert contacts > 20  # the episode really exercises wall contacts
+
+
+def test_rollout_until_done_teleport_matches_single_steps(gpu):
+    """pointmaze-teleport evaluation rollout: envs placed around the in-portals
+    so that many teleport inside the window; every written row (and the
+    out-portal each teleport picks, which follows the reset seed) equals K
+    single env.step calls (the rollout used a different key)."""
+    n, k = 4096, 12
+    rng = np.random.RandomState(23)
+    ins = np.array([[20.0, 12.0], [0.0, 16.0]])
+    centre = ins[np.arange(n) % 2]
+    ang = rng.uniform(0, 2 * np.pi, n)
+    q = centre + np.stack([np.cos(ang), np.sin(ang)], 1) * rng.uniform(0, 2.2, n)[:, None]
+    envs = [_env(gpu, n, 'teleport', max_episode_steps=150) for _ in range(2)]
+    for e in envs:
+        e.reset(seed=91, options=dict(task_id=1))
+        sd = e.state_dict()
+        sd['qpos'] = torch.tensor(q, device=gpu)
+        e.load_state_dict(sd)
+    acts = torch.tensor(rng.uniform(-1, 1, (k, n, 2)).astype(np.float32))
+    out = dict(obs=torch.zeros((k, n, 2), dtype=torch.float64, device=gpu),
+               reward=torch.zeros((k, n), dtype=torch.float32, device=gpu),
+               terminated=torch.zeros((k, n), dtype=torch.uint8, device=gpu),
+               truncated=torch.zeros((k, n), dtype=torch.uint8, device=gpu),
+               success=torch.zeros((k, n), dtype=torch.uint8, device=gpu),
+               steps=torch.zeros(n, dtype=torch.int32, device=gpu))
+    got = {key: v.cpu().numpy() for key, v in envs[0].rollout_until_done(acts, out).items()}
+    ref = dict(obs=[], reward=[], terminated=[], truncated=[], success=[])
+    for t in range(k):
+        o, r, te, tr, info = envs[1].step(acts[t])
+        for key, v in (('obs', o), ('reward', r), ('terminated', te), ('truncated', tr), ('success', info['success'])):
+            ref[key].append(v.cpu().numpy().copy())
+    ref = {key: np.stack(v) for key, v in ref.items()}
+    rows = np.arange(k)[:, None] < got['steps'][None, :]
+    for key in ('obs', 'reward', 'terminated', 'truncated', 'success'):
+        assert np.array_equal(got[key][rows], ref[key].astype(got[key].dtype)[rows]), key
+    qa, qb = envs[0].get_xy().cpu().numpy(), envs[1].get_xy().cpu().numpy()
+    alive = got['steps'] == k
+    assert np.array_equal(qa[alive], qb[alive])
+    outs = np.array([[24.0, 0.0], [0.0, 20.0], [36.0, 20.0]])
+    moved = (np.abs(qb[:, None, :] - outs[None]).max(-1) < 2.5).any(1)
+    assert moved.sum() > 200  # many envs went through a portal inside the window

@@ -9,7 +9,9 @@ truncated, success, final qpos) must be identical, and the all-gathered eval
 counters must equal the single-run counters.  pointmaze-large: 4096 envs x
 300 steps, expert actions with Philox noise, TimeLimit 250 with auto-reset;
 powderworld-easy: 128 envs x 30 steps with invalid actions (Philox
-replacements) and auto-reset.
+replacements) and auto-reset; antmaze-large wrapper (configs[4]): 1024 envs x
+60 steps on caller post-physics states, TimeLimit 25, auto-reset alternating
+caller reset states and Philox bodies, gathered eval counters.
 """
 
 import os
@@ -73,3 +75,20 @@ def test_powder_shards_equal_single_gpu_run(gpu, ranks):
         for k in ('obs', 'reward', 'terminated', 'truncated', 'success'):
             assert np.array_equal(got['powder_' + k], ref[k][:, b:b + n]), f'rank {r}: powder {k}'
     assert ref['truncated'].sum() > 0
+
+
+def test_ant_shards_equal_single_gpu_run(gpu, ranks):
+    ref, counters = sw.run_ant(0, sw.ANT_TOTAL, gpu)
+    per_env = ('obs0', 'goal0', 'body', 'goal_xy')
+    for r, got in enumerate(ranks):
+        b, n = int(got['abase']), int(got['an'])
+        for k in per_env + ('obs', 'final_obs', 'reward', 'terminated', 'truncated', 'success'):
+            exp = ref[k][b:b + n] if k in per_env else ref[k][:, b:b + n]
+            assert np.array_equal(got['ant_' + k], exp), f'rank {r}: ant {k} differs from the single run'
+    assert sum(int(g['an']) for g in ranks) == sw.ANT_TOTAL
+    for got in ranks:
+        assert np.array_equal(got['ant_gathered_total'], ref['counters'])
+        assert np.array_equal(got['ant_gathered_per_rank'].sum(0), ref['counters'])
+    # goal ends and TimeLimit ends both happen, so both reset paths ran
+    assert ref['terminated'].sum() > 100 and ref['truncated'].sum() > 100
+    assert ref['counters'][:, 0].sum() > 0
