@@ -277,7 +277,10 @@ typedef struct {
   int64_t row_bytes; /* bytes of one row (multiple of 4 uses dword copies) */
   int32_t select;    /* 0 = idxs, 1 = min(idxs+1, R-1) (next_observations,
                         datasets.py:82), 2 = value goal, 3 = actor goal */
-  int32_t pad_;
+  int32_t src_stride; /* bytes between consecutive source rows; 0 = row_bytes
+                        (dense).  A larger stride lets several small columns
+                        share one interleaved row record, so a sample's rows of
+                        them come from one 128-B line instead of one line each. */
 } ogbx_gc_column;
 
 /* Static description of an HBM-resident trajectory buffer. */
@@ -291,6 +294,10 @@ typedef struct {
                                 traj_end[valid_idxs]: lets a drawn index and its
                                 trajectory end load in parallel (NULL = two
                                 dependent loads)                                  */
+  const int64_t* valid_pairs; /* optional device [num_valid, 2] = (valid_idxs,
+                                valid_traj_end) interleaved: the drawn index and
+                                its trajectory end in ONE 16-B load (one line per
+                                pick instead of two); used when non-NULL         */
 } ogbx_gc_buffer;
 
 /* Goal-sampling configuration (GCDataset config keys, datasets.py:155-170).

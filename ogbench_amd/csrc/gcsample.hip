@@ -70,6 +70,10 @@ __device__ inline void index_loads(const ogbx_gc_buffer& buf, bool explicit_idxs
   const int64_t* __restrict__ vi = buf.valid_idxs;
   if (explicit_idxs) {
     *fin = buf.traj_end[*idx];
+  } else if (buf.valid_pairs) {
+    const longlong2 p = reinterpret_cast<const longlong2*>(buf.valid_pairs)[pick];
+    *idx = p.x;
+    *fin = p.y;
   } else if (vi && buf.valid_traj_end) {
     *idx = vi[pick];
     *fin = buf.valid_traj_end[pick];
@@ -83,7 +87,14 @@ __device__ inline void index_loads(const ogbx_gc_buffer& buf, bool explicit_idxs
 }
 
 __device__ inline int64_t rand_goal_of(const ogbx_gc_buffer& buf, int64_t pick) {
+  if (buf.valid_pairs) return buf.valid_pairs[2 * pick];
   return buf.valid_idxs ? buf.valid_idxs[pick] : pick;
+}
+
+// Source row pitch of a column in units of T (src_stride 0 = dense rows).
+template <typename T>
+__device__ __forceinline__ int64_t src_pitch(const ogbx_gc_column& col) {
+  return (col.src_stride ? (int64_t)col.src_stride : col.row_bytes) / (int64_t)sizeof(T);
 }
 
 __device__ inline int64_t geometric_from(double u, double log_q) {
@@ -96,6 +107,7 @@ template <typename T>
 __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, int64_t base,
                                  int tile) {
   const int64_t units = col.row_bytes / (int64_t)sizeof(T);
+  const int64_t pitch = src_pitch<T>(col);
   const T* __restrict__ src = (const T*)col.src;
   T* __restrict__ dst = (T*)col.dst;
   const int64_t total = units * tile;
@@ -103,7 +115,7 @@ __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, 
   int64_t b = threadIdx.x / units, k = threadIdx.x % units;
   const int64_t sb = step / units, sk = step % units;
   for (int64_t f = threadIdx.x; f < total; f += step) {
-    dst[(base + b) * units + k] = src[sel[b] * units + k];
+    dst[(base + b) * units + k] = src[sel[b] * pitch + k];
     k += sk;
     b += sb;
     if (k >= units) {
@@ -141,7 +153,7 @@ __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int6
           const int c = j / n_here, b = j - c * n_here;
           const ogbx_gc_column& col = cols.c[c];
           const int units = (int)(col.row_bytes >> 2);
-          const uint32_t* src = (const uint32_t*)col.src + sel[col.select][b] * units;
+          const uint32_t* src = (const uint32_t*)col.src + sel[col.select][b] * src_pitch<uint32_t>(col);
           uint32_t* dst = (uint32_t*)col.dst + (base + b) * units;
 #pragma unroll
           for (int q = 0; q < kSlots; ++q) {
@@ -164,7 +176,7 @@ __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int6
   for (int c = 0; c < num_cols; ++c) {
     const ogbx_gc_column& col = cols.c[c];
     const int64_t* srow = sel[col.select];
-    const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst;
+    const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst | (uintptr_t)col.src_stride;
     if (col.row_bytes % 16 == 0 && align % 16 == 0)
       copy_rows<uint4>(col, srow, base, n_here);
     else if (col.row_bytes % 8 == 0 && align % 8 == 0)
@@ -464,7 +476,9 @@ using namespace ogbx;
 static bool flat4_columns(const GcColumns& cc, int num_cols) {
   for (int i = 0; i < num_cols; ++i) {
     const ogbx_gc_column& c = cc.c[i];
-    if (c.row_bytes % 4 != 0 || c.row_bytes > 512 || ((uintptr_t)c.src | (uintptr_t)c.dst) % 4 != 0) return false;
+    if (c.row_bytes % 4 != 0 || c.row_bytes > 512 ||
+        ((uintptr_t)c.src | (uintptr_t)c.dst | (uintptr_t)c.src_stride) % 4 != 0)
+      return false;
   }
   return true;
 }
@@ -493,6 +507,8 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
              "no valid transitions in the dataset");
   GcColumns cc{};
   for (int i = 0; i < num_cols; ++i) {
+    OGBX_CHECK(cols[i].src_stride == 0 || cols[i].src_stride >= cols[i].row_bytes, OGBX_EINVAL,
+               "ogbx_gc_sample: src_stride below row_bytes");
     OGBX_CHECK(cols[i].src && cols[i].dst && cols[i].row_bytes > 0 && cols[i].select >= 0 &&
                    cols[i].select <= 3,
                OGBX_EINVAL, "ogbx_gc_sample: bad column descriptor");
@@ -548,6 +564,8 @@ ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg
              "no valid transitions in the dataset");
   GcColumns cc{};
   for (int i = 0; i < num_cols; ++i) {
+    OGBX_CHECK(cols[i].src_stride == 0 || cols[i].src_stride >= cols[i].row_bytes, OGBX_EINVAL,
+               "ogbx_gc_sample: src_stride below row_bytes");
     OGBX_CHECK(cols[i].src && cols[i].dst && cols[i].row_bytes > 0 && cols[i].select >= 0 &&
                    cols[i].select < kHgcSel,
                OGBX_EINVAL, "ogbx_hgc_sample: bad column descriptor");

@@ -237,6 +237,10 @@ __global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __res
 // k_steps.  Until then a done lane keeps stepping unobserved (as K single
 // steps would), so the wave's contact-path choice -- and with it every written
 // row -- is bit-identical to K calls of the single step.
+#ifdef OGBX_WAVE_STAMPS
+__device__ unsigned long long g_wave_stamps[4096 * 4];
+#endif
+
 template <bool kF64, bool kUntilDone>
 __global__ void __launch_bounds__(256) maze_step_kernel(
     const MazeParams* __restrict__ Pp, MazeState S, int64_t n, const void* __restrict__ action_v,
@@ -248,6 +252,9 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
   const MazeParams& P = *Pp;
   OGBX_POINT_MODEL(pm, P);
   __shared__ uint16_t nb_s[kMaxCells];
+#ifdef OGBX_WAVE_STAMPS
+  const unsigned long long ws_t0 = wall_clock64(), ws_c0 = clock64();
+#endif
   const int64_t i = env_of_lane(epw);
   const bool live = i >= 0 && i < n;
   // one HBM round trip before the first barrier: the wall-mask entry, the
@@ -372,6 +379,17 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     reinterpret_cast<double2*>(S.goal)[i] = make_double2(gx, gy);
     S.episode[i] = ep;
   }
+#ifdef OGBX_WAVE_STAMPS
+  {
+    const unsigned long long t1 = wall_clock64(), c1 = clock64();
+    const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0 && w < 4096) {
+      g_wave_stamps[4 * w + 0] = ws_t0;
+      g_wave_stamps[4 * w + 1] = t1;
+      g_wave_stamps[4 * w + 2] = c1 - ws_c0;
+    }
+  }
+#endif
 }
 
 template <bool kF64>
@@ -803,6 +821,22 @@ ogbx_status ogbx_diag_phys_stamps(unsigned long long* out) {
   OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phys_stamps), 4096 * 4 * sizeof(unsigned long long)));
   static unsigned long long z[4096 * 4];
   OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phys_stamps), z, sizeof(z)));
+  return OGBX_OK;
+}
+#endif
+
+#ifdef OGBX_WAVE_STAMPS
+// Diagnostic build only: per-wave (start, end) wall clock (s_memrealtime,
+// 100 MHz) and shader-clock cycles of the last maze_step_kernel launch.
+ogbx_status ogbx_diag_wave_stamps(unsigned long long* out) {
+  OGBX_HIP(hipDeviceSynchronize());
+  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_stamps), 4096 * 4 * sizeof(unsigned long long)));
+  // slot 3: the path counters of point_physics.h g_wave_paths (then cleared)
+  static unsigned long long paths[4096];
+  OGBX_HIP(hipMemcpyFromSymbol(paths, HIP_SYMBOL(g_wave_paths), sizeof(paths)));
+  for (int w = 0; w < 4096; ++w) out[4 * w + 3] = paths[w];
+  static unsigned long long z[4096];
+  OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_paths), z, sizeof(z)));
   return OGBX_OK;
 }
 #endif

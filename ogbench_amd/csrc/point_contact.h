@@ -461,6 +461,316 @@ __device__ __forceinline__ void contact_loop(const PointModel& pm, const uint16_
   *bail = bl;
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined lean loop (default lean form; -DOGBX_LEAN_SERIAL restores
+// contact_loop<true>).
+//
+// In the RK4 stage loop the NEXT stage's position never depends on the current
+// stage's solve: qs(e+1) = x + h cf vs(e) inside a substep and x + h sum(b vs)
+// at its end, both known before the acceleration of stage e.  So stage e+1's
+// collision runs beside stage e's solve, and the two rare per-stage paths --
+// an active set that changes (stage e) and an impedance-band contact (stage
+// e+1) -- share ONE wave-uniform branch per stage instead of a branch in each
+// half.  One basic block per stage gives the scheduler two independent fp64
+// chains to interleave; serial, every branch drained the pipeline between
+// collision and solve.
+//
+// The lookahead collider keeps the role layout with the side of every role
+// fixed for the step: sx = sign(lx), sy = sign(ly) of the first stage's
+// centre (the face normals are then (-sx, 0) and (0, -sy) for the whole step).
+// That equals collide_roles' choice at every stage: where collide_roles picks
+// side 0 (|l| < h - r) the fixed side's face and corner are out of reach
+// (dist > 1e-9), so both see no contact there.  The face distance is
+// (h - sx lx) - r, the corner distance sqrt(ex^2 + ey^2) - r with ex = h - sx lx;
+// both equal collide_roles' to rounding.  (The first stage -- whose contact
+// flag is the reported one -- still comes from the exact stage_contacts.)
+// A lane bails to the full loop when its centre leaves the inner part of its
+// cell (|l| >= h) or crosses to the far side of its step-start half
+// (sx lx <= -1.25, never reachable in a step: contacts move the centre by a
+// fraction of their penetration), or when its active set does not settle in
+// OGBX_LEAN_ITERS iterations.
+struct LeanSides {
+  double cx, cy, sxd, syd;
+  // per-side radius: r where the side holds a wall, -1e3 where it does not
+  // (the distance is then far positive: no contact, no compare against the
+  // wall bit); rD likewise and the corner's squared-distance bound
+  double rX, rY, rD, farD2;
+  double wX, wY, wD;  // w_max on a wall side, 0 elsewhere
+  uint32_t bX, bY, bD;  // the slot's edge bits on a wall side
+};
+
+__device__ __forceinline__ LeanSides lean_sides(const PointModel& pm, const RoleFrame& fr, double x, double y) {
+  LeanSides L;
+  L.cx = fr.cx;
+  L.cy = fr.cy;
+  const bool px = x - fr.cx >= 0.0, py = y - fr.cy >= 0.0;
+  L.sxd = px ? 1.0 : -1.0;
+  L.syd = py ? 1.0 : -1.0;
+  const int sx = px ? 1 : -1, sy = py ? 1 : -1;
+  const bool vX = (fr.m >> (4 + sx)) & 1u, vY = (fr.m >> (4 + 3 * sy)) & 1u, vD = (fr.m >> (4 + 3 * sy + sx)) & 1u;
+  L.rX = vX ? pm.radius : -1e3;
+  L.rY = vY ? pm.radius : -1e3;
+  L.rD = vD ? pm.radius : -1e3;
+  L.farD2 = vD ? kPointFarD2 : -1.0;
+  L.wX = vX ? pm.w_max : 0.0;
+  L.wY = vY ? pm.w_max : 0.0;
+  L.wD = vD ? pm.w_max : 0.0;
+  L.bX = vX ? kSlotBits : 0u;
+  L.bY = vY ? kSlotBits << 3 : 0u;
+  L.bD = vD ? kSlotBits << 6 : 0u;
+  return L;
+}
+
+// Distances of the three role slots at (x, y).  emin/emax track the smallest
+// and largest face offset e = h - s l over the step (bail test at the end:
+// every stage needs 0 < e < h + 1.25).
+struct LeanHit {
+  double d0, d1, d2, ex, ey, inv;
+  bool cX, cY, cD, band;
+};
+
+__device__ __forceinline__ void lean_collide(const PointModel& pm, const LeanSides& L, double x, double y,
+                                             LeanHit& k, double& emin, double& emax) {
+  const double hx = pm.box_hxy;
+  const double lx = x - L.cx, ly = y - L.cy;
+  k.ex = fma(-L.sxd, lx, hx);  // h - sx lx (sx = +-1: one rounding)
+  k.ey = fma(-L.syd, ly, hx);
+  emin = fmin(emin, fmin(k.ex, k.ey));
+  emax = fmax(emax, fmax(k.ex, k.ey));
+  k.d0 = k.ex - L.rX;
+  k.d1 = k.ey - L.rY;
+  const double d2 = fma(k.ex, k.ex, k.ey * k.ey);
+  k.cX = k.d0 <= 0.0;
+  k.cY = k.d1 <= 0.0;
+  k.cD = !(d2 > L.farD2);
+  // e > 0 on both axes at every kept stage, so d2 > 0 (a lane with e <= 0
+  // bails and its values here are discarded)
+  const double y0 = __builtin_amdgcn_rsq(d2);
+  k.inv = y0 * fma(-0.5 * d2 * y0, y0, 1.5);
+  k.d2 = d2 * k.inv - L.rD;
+#ifdef OGBX_BAND_BRANCH
+  // impedance band, conservatively wide (contact_gains decides exactly)
+  const double n0 = k.cX ? k.d0 : -1.0, n1 = k.cY ? k.d1 : -1.0, n2 = k.cD ? k.d2 : -1.0;
+  k.band = fmax(n0, fmax(n1, n2)) > -1.0001 * pm.imp_width;
+#else
+  k.band = false;  // the gains of lean_slots cover the band
+#endif
+}
+
+// Impedance gains of one slot without a branch or a band test
+// (-DOGBX_BAND_BRANCH restores the wave-uniform band branch): with
+// x = min(|d| / width, 1), the power-2 sigmoid of solimp (mid 0.5) is
+// y = 2 x^2 - max(0, 2 x - 1)^2, imp = dmin + (dmax - dmin) y, and with
+// u = 1 - imp the gains are D = imp / (u diag) = (1/u - 1) / diag and
+// kp = K imp d.  Outside the band (x = 1) they are w_max and kp_max d to an
+// ulp.  The per-wave tail of a step is waves with a contact resting inside
+// the band (|d| < 1 mm) at every stage, so the band computation is part of
+// every stage rather than a branch those waves take 20 times.
+static_assert(kPointModel.imp_mid == 0.5 && kPointModel.imp_a == 2.0 && kPointModel.imp_b == 2.0,
+              "band_u assumes the default solimp midpoint and power");
+__device__ __forceinline__ double band_u(const PointModel& pm, double d) {
+  const double x = fmin(fabs(d) * pm.inv_width, 1.0);
+  const double m = fmax(fma(2.0, x, -1.0), 0.0);
+  const double y = fma(2.0 * x, x, -(m * m));
+  return fma(-(pm.imp_dmax - pm.imp_dmin), y, 1.0 - pm.imp_dmin);
+}
+
+__device__ __forceinline__ uint32_t lean_slots(const PointModel& pm, const LeanSides& L, const LeanHit& k,
+                                               Contacts& c) {
+  c.s0.nx = -L.sxd;
+  c.s0.ny = 0.0;
+  c.s1.nx = 0.0;
+  c.s1.ny = -L.syd;
+  c.s2.nx = -L.sxd * (k.ex * k.inv);
+  c.s2.ny = -L.syd * (k.ey * k.inv);
+#ifndef OGBX_BAND_BRANCH
+  const double u0 = band_u(pm, k.d0), u1 = band_u(pm, k.d1), u2 = band_u(pm, k.d2);
+  // one reciprocal for the three: 1/(u0 u1 u2), two Newton-Raphson steps
+  const double p01 = u0 * u1, p = p01 * u2;
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  r = fma(r, fma(-p, r, 1.0), r);
+  const double r01 = r * u2;  // 1 / (u0 u1)
+  const double idg = 1.0 / pm.diag;
+  c.s0.w = k.cX ? fma(r01 * u1, idg, -idg) : 0.0;
+  c.s1.w = k.cY ? fma(r01 * u0, idg, -idg) : 0.0;
+  c.s2.w = k.cD ? fma(r * p01, idg, -idg) : 0.0;
+  c.s0.kp = fma(-u0, pm.K, pm.K) * k.d0;
+  c.s1.kp = fma(-u1, pm.K, pm.K) * k.d1;
+  c.s2.kp = fma(-u2, pm.K, pm.K) * k.d2;
+#else
+  c.s0.kp = pm.kp_max * k.d0;
+  c.s1.kp = pm.kp_max * k.d1;
+  c.s2.kp = pm.kp_max * k.d2;
+  c.s0.w = k.cX ? L.wX : 0.0;
+  c.s1.w = k.cY ? L.wY : 0.0;
+  c.s2.w = k.cD ? L.wD : 0.0;
+#endif
+  c.n = 0;  // unused by the role evaluation
+  c.roles = true;
+  return (k.cX ? L.bX : 0u) | (k.cY ? L.bY : 0u) | (k.cD ? L.bD : 0u);
+}
+
+// Impedance-band gains of all three slots, branch free (contact_gains without
+// its branches; the per-wave tail of the step is waves with a contact resting
+// inside the band at every stage, so this path is hot for them).  The three
+// quotients imp / ((1 - imp) diag) share one v_rcp_f64 (1/(a b c), two
+// Newton-Raphson refinements, then 1/a = (b c)/(a b c) ...): a few ulp from
+// the IEEE division (contact tolerance 1e-9).
+__device__ __forceinline__ void band_imp(const PointModel& pm, double d, double& imp, double& den, bool& inb) {
+  const double x = fabs(d) * pm.inv_width;
+  inb = x < 1.0;
+  const double xc = fmin(x, 1.0);
+  const double lo = pm.imp_a * (xc * xc);
+  const double hi = 1.0 - pm.imp_b * ((1.0 - xc) * (1.0 - xc));
+  const double yv = xc <= pm.imp_mid ? lo : hi;
+  imp = pm.imp_dmin + yv * (pm.imp_dmax - pm.imp_dmin);  // x = 0: y = 0, imp = dmin
+  den = (1.0 - imp) * pm.diag;
+}
+
+__device__ __forceinline__ void lean_band(const PointModel& pm, const LeanHit& k, Contacts& c) {
+  double i0, i1, i2, a0, a1, a2;
+  bool b0, b1, b2;
+  band_imp(pm, k.d0, i0, a0, b0);
+  band_imp(pm, k.d1, i1, a1, b1);
+  band_imp(pm, k.d2, i2, a2, b2);
+  b0 &= c.s0.w != 0.0;
+  b1 &= c.s1.w != 0.0;
+  b2 &= c.s2.w != 0.0;
+  const double p01 = a0 * a1, p = p01 * a2;
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  r = fma(r, fma(-p, r, 1.0), r);
+  const double r01 = r * a2;  // 1 / (a0 a1)
+  c.s0.w = b0 ? i0 * (r01 * a1) : c.s0.w;
+  c.s1.w = b1 ? i1 * (r01 * a0) : c.s1.w;
+  c.s2.w = b2 ? i2 * (r * p01) : c.s2.w;
+  c.s0.kp = b0 ? pm.K * i0 * k.d0 : c.s0.kp;
+  c.s1.kp = b1 ? pm.K * i1 * k.d1 : c.s1.kp;
+  c.s2.kp = b2 ? pm.K * i2 * k.d2 : c.s2.kp;
+}
+
+
+#ifdef OGBX_WAVE_STAMPS
+__device__ unsigned long long g_wave_paths[4096];
+#endif
+
+__device__ __forceinline__ void contact_loop_pipe(const PointModel& pm, double& x, double& y, const RoleFrame& fr,
+                                                  Contacts c, uint32_t valid, bool* bail) {
+  bool bl = false;
+#ifdef OGBX_WAVE_STAMPS
+  unsigned long long g_wpath = 0;
+#endif
+  const double h = pm.h;
+  const LeanSides L = lean_sides(pm, fr, x, y);
+  double emin = pm.box_hxy, emax = pm.box_hxy;
+  double vx = 0.0, vy = 0.0, vsx = 0.0, vsy = 0.0;
+  double sqx = 0.0, sqy = 0.0, svx = 0.0, svy = 0.0;
+  uint32_t act = edge_mask<true>(c, 0.0, 0.0) & valid;
+  PieceWeights pw;
+  piece_weights(act, pw);
+  const double mB = pm.mass * pm.B;
+  const int nstage = 4 * pm.nsub;
+#pragma unroll OGBX_AS_UNROLL
+  for (int e = 0; e < nstage; ++e) {
+    const int st = e & 3;
+    const bool more = e + 1 < nstage;
+    // the next stage's position (independent of this stage's solve)
+    double nqx, nqy, nsqx, nsqy, nx_ = x, ny_ = y;
+    {
+#pragma clang fp contract(fast)
+      const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
+      nsqx = sqx + b * vsx;
+      nsqy = sqy + b * vsy;
+      if (st < 3) {
+        const double cf = (st < 2) ? 0.5 : 1.0;
+        nqx = x + h * (cf * vsx);
+        nqy = y + h * (cf * vsy);
+      } else {
+        nx_ = x + h * nsqx;
+        ny_ = y + h * nsqy;
+        nqx = nx_;
+        nqy = ny_;
+      }
+    }
+    // lookahead collision of stage e+1
+    LeanHit k;
+    bool band_next = false;
+    if (more) {
+      lean_collide(pm, L, nqx, nqy, k, emin, emax);
+      band_next = k.band;
+    }
+    // stage e: one build + solve + mask from the warm-started active set
+    double ux, uy;
+    const double mbvx = mB * vsx, mbvy = mB * vsy;
+    piece_min<true>(pm, c, pw, mbvx, mbvy, &ux, &uy);
+    uint32_t A2 = edge_mask<true>(c, ux, uy);
+    bool done = ((A2 ^ act) & valid) == 0u;
+    Contacts cn;
+    uint32_t valid_n = 0u;
+    if (more) valid_n = lean_slots(pm, L, k, cn);
+    OGBX_WSTAT(9, true);
+    OGBX_WSTAT(13, !done);
+    OGBX_WSTAT(10, band_next);
+#ifdef OGBX_ABL_PIPE_NOITER
+    done = true;  // timing-only ablation: no active-set iteration (changes the physics)
+#endif
+    if (__builtin_expect(__any(!done | band_next), 0)) {
+      OGBX_WPATH(0);
+      if (__any(band_next)) OGBX_WPATH(40);
+      if (__any(!done)) {
+#pragma unroll 1
+        for (int it = 0; it < OGBX_LEAN_ITERS && !done; ++it) {
+          OGBX_WPATH(20);
+          act = A2 & valid;
+          piece_weights(act, pw);
+          piece_min<true>(pm, c, pw, mbvx, mbvy, &ux, &uy);
+          A2 = edge_mask<true>(c, ux, uy);
+          done = ((A2 ^ act) & valid) == 0u;
+        }
+        bl |= !done;
+      }
+      if (more && __any(band_next)) lean_band(pm, k, cn);
+    }
+    double fx, fy;
+    {
+#pragma clang fp contract(fast)
+      fx = ux - pm.B * vsx;
+      fy = uy - pm.B * vsy;
+      const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
+      svx = svx + b * fx;
+      svy = svy + b * fy;
+      if (st < 3) {
+        const double cf = (st < 2) ? 0.5 : 1.0;
+        sqx = nsqx;
+        sqy = nsqy;
+        vsx = vx + (cf * fx) * h;
+        vsy = vy + (cf * fy) * h;
+      } else {
+        vx = vx + svx * h;
+        vy = vy + svy * h;
+        x = nx_;
+        y = ny_;
+        vsx = vx;
+        vsy = vy;
+        sqx = sqy = svx = svy = 0.0;
+      }
+    }
+    if (more) {
+      c = cn;
+      valid = valid_n;
+    }
+  }
+  *bail = bl | !(emin > 0.0) | !(emax < pm.box_hxy + 1.25);
+#ifdef OGBX_WAVE_STAMPS
+  {
+    const unsigned long long b = __ballot(1);
+    const unsigned w = (unsigned)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (w < 4096 && (int)(threadIdx.x & 63) == __ffsll((long long)b) - 1) g_wave_paths[w] = g_wpath;
+  }
+#endif
+}
+
 // One PointEnv physics step (same RK4 loop as point_physics.h point_step).
 __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_t* wall, int H, int W,
                                              double* px, double* py) {
@@ -482,7 +792,11 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
   const double x0 = x, y0 = y;
 #ifndef OGBX_NO_LEAN_SPLIT
   bool bail = true;
+#ifndef OGBX_LEAN_SERIAL
+  if (!__any(generic)) contact_loop_pipe(pm, x, y, fr, c, valid, &bail);
+#else
   if (!__any(generic)) contact_loop<true>(pm, wall, H, W, x, y, fr, c, valid, false, &bail);
+#endif
   OGBX_WSTAT(14, bail);
   if (__builtin_expect(__any(bail), 0)) {
     // redo the step with the full loop from the same first stage

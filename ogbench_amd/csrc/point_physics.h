@@ -108,6 +108,16 @@ __device__ __forceinline__ unsigned long long stamp() {
 #define OGBX_STAMP_END ((void)0)
 #endif
 
+#ifdef OGBX_WAVE_STAMPS
+// Diagnostic build only: per-wave path counters of the current step, packed
+// [cold-block entries | iteration trips << 20 | band stages << 40], kept in a
+// register (no memory traffic on the measured path) and stored with the
+// wave's time stamps at the end of maze_step_kernel.
+#define OGBX_WPATH(shift) (g_wpath += 1ull << (shift))
+#else
+#define OGBX_WPATH(shift) ((void)0)
+#endif
+
 #ifdef OGBX_PHYS_STATS
 // Diagnostic build only (-DOGBX_PHYS_STATS): per-path counters.
 __device__ unsigned long long g_phys_stats[16];

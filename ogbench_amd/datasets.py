@@ -38,7 +38,7 @@ class GcColumn(ctypes.Structure):
         ('dst', ctypes.c_void_p),
         ('row_bytes', ctypes.c_int64),
         ('select', ctypes.c_int32),
-        ('pad_', ctypes.c_int32),
+        ('src_stride', ctypes.c_int32),
     ]
 
 
@@ -49,6 +49,7 @@ class GcBuffer(ctypes.Structure):
         ('num_valid', ctypes.c_int64),
         ('traj_end', ctypes.c_void_p),
         ('valid_traj_end', ctypes.c_void_p),
+        ('valid_pairs', ctypes.c_void_p),
     ]
 
 
@@ -234,10 +235,14 @@ class GCDataset:
         valid = getattr(dataset, 'valid_idxs', None)
         # trajectory end of every valid row: the drawn index and its end load in parallel
         self.valid_traj_end = self.traj_end[valid].contiguous() if valid is not None else None
+        # (index, trajectory end) of every valid row interleaved: one 16-B load per pick
+        self.valid_pairs = torch.stack([valid, self.valid_traj_end], 1).contiguous() if valid is not None else None
         self._buf = GcBuffer(self.size, valid.data_ptr() if valid is not None else None,
                              valid.numel() if valid is not None else 0, self.traj_end.data_ptr(),
-                             self.valid_traj_end.data_ptr() if valid is not None else None)
+                             self.valid_traj_end.data_ptr() if valid is not None else None,
+                             self.valid_pairs.data_ptr() if valid is not None else None)
         self._valid = valid
+        self._record, self._rec_off = self._row_record(dataset)
 
         def thresh(p_traj, p_cur):
             return p_traj / (1.0 - p_cur) if p_cur != 1.0 else 0.0  # datasets.py:321
@@ -255,6 +260,44 @@ class GCDataset:
         self._out_cache = {}
 
     # ---------------------------------------------------------------- helpers
+    _RECORD_BYTES = 128  # one L2 line
+
+    def _row_record(self, ds):
+        """The sampler's own interleaved copy of the dataset's small columns
+        (every key but the goal sources whose row is 4-byte granular, packed in
+        key order while they fit one 128-B line per row, e.g. actions 84 +
+        terminals 4 + valids 4 of the humanoid layout): a sample's rows of them
+        then come from one line of HBM instead of one line per column.  The
+        dataset's own tensors (and the returned batch) keep the reference
+        shapes.  None when fewer than two columns fit."""
+        torch = _torch()
+        goal_srcs = {'observations', 'oracle_reps'}
+        off, picks = 0, []
+        for k, v in ds.items():
+            if k in goal_srcs:
+                continue
+            rb = (v[0].numel() if v.dim() > 1 else 1) * v.element_size()
+            if rb % 4 or off + rb > self._RECORD_BYTES:
+                continue
+            picks.append((k, off, rb))
+            off += rb
+        if len(picks) < 2:
+            return None, {}
+        rec = torch.zeros(self.size, self._RECORD_BYTES, dtype=torch.uint8, device=self.device)
+        for k, o, rb in picks:
+            rec[:, o:o + rb] = ds[k].reshape(self.size, -1).contiguous().view(torch.uint8)
+        return rec, {k: o for k, o, _ in picks}
+
+    def _column(self, src_key, dst, select):
+        """Descriptor of one gathered column (from the row record when the key
+        lives there)."""
+        src = self.dataset[src_key]
+        row_bytes = src[0].numel() * src.element_size() if src.dim() > 1 else src.element_size()
+        o = self._rec_off.get(src_key)
+        if o is not None:
+            return GcColumn(self._record.data_ptr() + o, dst.data_ptr(), row_bytes, select, self._RECORD_BYTES)
+        return GcColumn(src.data_ptr(), dst.data_ptr(), row_bytes, select, 0)
+
     def _p_aug_draw(self, out, evaluation):
         # p_aug draw (datasets.py:278-279): image crops apply only to 4-D arrays
         p_aug = self.config.get('p_aug')
@@ -278,9 +321,8 @@ class GCDataset:
         def add(src_key, dst_key, select):
             src = ds[src_key]
             dst = torch.empty((total,) + tuple(src.shape[1:]), dtype=src.dtype, device=self.device)
-            row_bytes = src[0].numel() * src.element_size() if src.dim() > 1 else src.element_size()
             out[dst_key] = dst
-            cols.append(GcColumn(src.data_ptr(), dst.data_ptr(), row_bytes, select, 0))
+            cols.append(self._column(src_key, dst, select))
 
         for k in (ds.keys() if keys is None else keys):
             add(k, k, 0)
@@ -482,8 +524,7 @@ class HGCDataset(GCDataset):
         def col(src_key, select):
             src = ds[src_key]
             dst = torch.empty((total,) + tuple(src.shape[1:]), dtype=src.dtype, device=self.device)
-            row_bytes = src[0].numel() * src.element_size() if src.dim() > 1 else src.element_size()
-            cols.append(GcColumn(src.data_ptr(), dst.data_ptr(), row_bytes, select, 0))
+            cols.append(self._column(src_key, dst, select))
             return dst
 
         def scalar(dtype):

@@ -121,7 +121,7 @@ class MazeEnv:
         self._noise = 1
         self._goal_tol = 1.0 if loco_env_type == 'point' else 0.5
         self.max_episode_steps = int(max_episode_steps)
-        self.auto_reset = bool(auto_reset)
+        self._auto_i = int(bool(auto_reset))
 
         opts = _lib.MazeOpts(
             loco_type=LOCO_TYPES[loco_env_type],
@@ -139,6 +139,7 @@ class MazeEnv:
             _lib.check(L.ogbx_maze_create(maze_type.encode(), self.num_envs, self.device.index, opts, h))
         self._h = h
         self._L = L
+        self._wrap_fn = L.ogbx_antmaze_step
 
         self.maze_map, tasks = static_tables(maze_type)
         self.task_infos = []
@@ -184,10 +185,20 @@ class MazeEnv:
         self._term_b = self._term.view(torch.bool)
         self._trunc_b = self._trunc.view(torch.bool)
         self._succ_b = self._succ.view(torch.bool)
+        self._wrap_cache = {}
+        self._dev_idx = self.device.index
         self._seed = None
         self._init_seed = seed
         self._has_reset = False
         self.cur_task_id = None
+
+    @property
+    def auto_reset(self):
+        return bool(self._auto_i)
+
+    @auto_reset.setter
+    def auto_reset(self, value):
+        self._auto_i = int(bool(value))
 
     # ------------------------------------------------------------ lifecycle
     def close(self):
@@ -500,30 +511,50 @@ class MazeEnv:
         Returns (obs [N,29], reward, terminated, truncated, info{'success'}) as
         ``step`` does; with auto_reset, ``reset_states`` [N,29] (optional) are
         the caller's reset states for the envs that end (xy := init_xy)."""
-        if self._loco_env_type != 'ant':
-            raise ValueError('wrap_step() is for ant handles; point envs use step(action)')
-        # per-call host cost matters here (a 16k-env launch is ~5 us): one
-        # combined layout check, raw pointers, the cached output pointers
-        q = qpos if qpos.is_contiguous() else qpos.contiguous()
-        v = qvel if qvel.is_contiguous() else qvel.contiguous()
-        if (q.shape != self._ant_qshape or v.shape != self._ant_vshape or q.dtype != self._f64 or v.dtype != self._f64
-                or q.get_device() != self.device.index or v.get_device() != self.device.index):
-            raise ValueError(f'wrap_step: qpos/qvel must be float64 {tuple(self._ant_qshape)}/{tuple(self._ant_vshape)} '
-                             f'on {self.device}')
+        # Per-call host cost matters here (a 16k-env launch is ~5 us).  Fast
+        # path: a (qpos, qvel) pair seen before -- the handle's own body_state()
+        # views of an in-place engine, or a fixed ring of state buffers -- skips
+        # every layout check and pointer lookup: the pair's validated raw
+        # pointers are cached by tensor identity (the cache holds the tensors,
+        # so their ids stay unique while cached).  Anything else takes the
+        # checked path once and is cached.
         rs = None
         if reset_states is not None:
             torch = _torch()
             rs = torch.as_tensor(reset_states).to(self.device, torch.float64).contiguous()
             assert rs.shape == (self.num_envs, 29)
             rs = rs.data_ptr()
-        st = self._L.ogbx_antmaze_step(self._h, q.data_ptr(), v.data_ptr(), *self._step_out, int(self.auto_reset), rs,
-                                       _lib.stream_of(self.device))
+        hit = self._wrap_cache.get((id(qpos), id(qvel)))
+        if hit is not None and hit[0] is qpos and hit[1] is qvel:
+            qp, vp = hit[2], hit[3]
+        else:
+            qp, vp = self._wrap_validate(qpos, qvel)
+        st = self._wrap_fn(self._h, qp, vp, *self._step_out, self._auto_i, rs, _raw_stream(self._dev_idx))
         if st != 0:
             _lib.check(st, 'wrap_step')
         info = {'success': self._succ_b}
         if self.auto_reset:
             info['final_observation'] = self._final_obs
         return self._obs, self._reward, self._term_b, self._trunc_b, info
+
+    def _wrap_validate(self, qpos, qvel):
+        if self._loco_env_type != 'ant':
+            raise ValueError('wrap_step() is for ant handles; point envs use step(action)')
+        q, v = qpos, qvel
+        if (q.shape != self._ant_qshape or v.shape != self._ant_vshape or q.dtype != self._f64 or v.dtype != self._f64
+                or q.get_device() != self.device.index or v.get_device() != self.device.index):
+            raise ValueError(f'wrap_step: qpos/qvel must be float64 {tuple(self._ant_qshape)}/{tuple(self._ant_vshape)} '
+                             f'on {self.device}')
+        if not (q.is_contiguous() and v.is_contiguous()):
+            # a strided pair is copied each call, never cached; the copies stay
+            # referenced by the handle until the next such call, past the launch
+            self._wrap_tmp = (q.contiguous(), v.contiguous())
+            return self._wrap_tmp[0].data_ptr(), self._wrap_tmp[1].data_ptr()
+        if len(self._wrap_cache) >= 32:
+            self._wrap_cache.clear()
+        qp, vp = q.data_ptr(), v.data_ptr()
+        self._wrap_cache[(id(q), id(v))] = (q, v, qp, vp)
+        return qp, vp
 
     def rollout(self, actions, out=None):
         """K fused steps in ONE launch: actions [K,N,2] -> per-step outputs [K,N,...].
@@ -636,6 +667,13 @@ def _zero_episodes(episode, mask, device):
     else:
         m = _torch().as_tensor(mask).to(device).bool().reshape(-1)
         episode.masked_fill_(m, 0)
+
+
+def _raw_stream(device_index):
+    """hipStream_t (as an int) of torch's current stream on device_index."""
+    global _raw_stream
+    _raw_stream = _torch()._C._cuda_getCurrentRawStream  # bind once
+    return _raw_stream(device_index)
 
 
 def _from_ptr(addr, shape, dtype, device):

@@ -14,13 +14,14 @@ ROUND=${ROUND:-r01}
 STEPS=${STEPS:-300}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-ARGS="--workload $WL --steps $STEPS --warmup ${WARMUP:-100} --no-cpu-baseline --no-extras"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$WL -o run --output-format csv -- \
-  python3 bench.py $ARGS > gpurun_out/prof_${WL}.log 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$WL -o run --output-format csv -- \
-  python3 bench.py $ARGS > gpurun_out/pmc_fetch_${WL}.log 2>&1 || exit $?
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$WL -o run --output-format csv -- \
-  python3 bench.py $ARGS > gpurun_out/pmc_write_${WL}.log 2>&1 || exit $?
-tail -1 gpurun_out/prof_${WL}.log
+ARGS="--workload $WL --steps $STEPS --warmup ${WARMUP:-100} --no-cpu-baseline --no-extras ${BENCH_ARGS:-}"
+TAG=${TAG:-$WL}
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
+  python3 bench.py $ARGS > gpurun_out/prof_${TAG}.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- \
+  python3 bench.py $ARGS > gpurun_out/pmc_fetch_${TAG}.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- \
+  python3 bench.py $ARGS > gpurun_out/pmc_write_${TAG}.log 2>&1 || exit $?
+tail -1 gpurun_out/prof_${TAG}.log
 # profiles/ is written back here (gpurun returns only gpurun_out/):
 #   python3 scripts/prof_summary.py --round $ROUND --workload $WL --kernel $KERNEL

@@ -36,4 +36,5 @@ for i in range(300):
 torch.cuda.synchronize()
 L.ogbx_diag_phys_stats(buf)
 s = list(buf)
-print(f'bench 300 steps: contact wave-stages {s[9]} bail waves {s[14]} slow wave-stages {s[12]}', flush=True)
+print(f'bench 300 steps: contact wave-stages {s[9]} bail waves {s[14]} slow wave-stages {s[12]} '
+      f'iterating wave-stages {s[13]} band wave-stages {s[10]}', flush=True)

@@ -179,3 +179,33 @@ def test_point_only_entry_points_refuse_ant(gpu):
         env.step(torch.zeros(4, 8))
     with pytest.raises(ValueError):
         ogbench_amd.MazeEnv('point', 'large', num_envs=4, device=gpu).body_state()
+
+
+def test_wrap_step_cached_and_strided_inputs(gpu):
+    """wrap_step's cached fast path (same tensors every call, contents changed
+    in place) and the checked path (strided views, copied; bad shapes raise)
+    give the same outputs as fresh contiguous tensors."""
+    n = 256
+    rng = np.random.RandomState(4)
+    a, b = _env(gpu, n, 'post'), _env(gpu, n, 'post')
+    for e in (a, b):
+        e.reset(seed=2, options=dict(task_id=3))
+    qbuf = torch.zeros(n, 15, dtype=torch.float64, device=gpu)
+    vbuf = torch.zeros(n, 14, dtype=torch.float64, device=gpu)
+    for t in range(6):
+        q = torch.tensor(rng.normal(size=(n, 15)), device=gpu)
+        v = torch.tensor(rng.normal(size=(n, 14)), device=gpu)
+        qbuf.copy_(q)
+        vbuf.copy_(v)
+        wide = torch.zeros(n, 40, dtype=torch.float64, device=gpu)
+        wide[:, :15] = q
+        wide[:, 20:34] = v
+        got = a.wrap_step(qbuf, vbuf) if t % 2 == 0 else a.wrap_step(wide[:, :15], wide[:, 20:34])
+        got = [x.cpu().numpy().copy() for x in got[:4]]
+        exp = [x.cpu().numpy().copy() for x in b.wrap_step(q.clone(), v.clone())[:4]]
+        for g_, e_ in zip(got, exp):
+            assert np.array_equal(g_, e_), t
+    with pytest.raises(ValueError):
+        a.wrap_step(qbuf[:, :14], vbuf)
+    with pytest.raises(ValueError):
+        a.wrap_step(qbuf.float(), vbuf)
