@@ -842,11 +842,11 @@ ogbx_status ogbx_diag_wave_stamps(unsigned long long* out) {
 #endif
 
 #ifdef OGBX_PHYS_STATS
-// Diagnostic build only: read and clear the 16 physics path counters.
+// Diagnostic build only: read and clear the 32 physics path counters.
 ogbx_status ogbx_diag_phys_stats(unsigned long long* out16) {
   OGBX_HIP(hipDeviceSynchronize());
-  OGBX_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phys_stats), 16 * sizeof(unsigned long long)));
-  unsigned long long z[16] = {0};
+  OGBX_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phys_stats), 32 * sizeof(unsigned long long)));
+  unsigned long long z[32] = {0};
   OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phys_stats), z, sizeof(z)));
   return OGBX_OK;
 }

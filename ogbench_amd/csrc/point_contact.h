@@ -671,6 +671,9 @@ __device__ __forceinline__ void contact_loop_pipe(const PointModel& pm, double& 
   piece_weights(act, pw);
   const double mB = pm.mass * pm.B;
   const int nstage = 4 * pm.nsub;
+#ifdef OGBX_PHYS_STATS
+  uint32_t valid_prev = valid;
+#endif
 #pragma unroll OGBX_AS_UNROLL
   for (int e = 0; e < nstage; ++e) {
     const int st = e & 3;
@@ -696,24 +699,68 @@ __device__ __forceinline__ void contact_loop_pipe(const PointModel& pm, double& 
     // lookahead collision of stage e+1
     LeanHit k;
     bool band_next = false;
+#ifndef OGBX_PIPE_CHECK_FIRST
     if (more) {
       lean_collide(pm, L, nqx, nqy, k, emin, emax);
       band_next = k.band;
     }
+#endif
     // stage e: one build + solve + mask from the warm-started active set
     double ux, uy;
     const double mbvx = mB * vsx, mbvy = mB * vsy;
     piece_min<true>(pm, c, pw, mbvx, mbvy, &ux, &uy);
     uint32_t A2 = edge_mask<true>(c, ux, uy);
+#ifndef OGBX_NO_FIRST_TRIP
+    if (e == 0) {
+      // The first stage's warm start (every penetrating edge active) is exact
+      // for a single contact but wrong for about half of the multi-contact
+      // lanes (53 % of all active-set iterations of a step were this stage's):
+      // one semismooth Newton step for every lane here, in line.
+      act = A2 & valid;
+      piece_weights(act, pw);
+      piece_min<true>(pm, c, pw, mbvx, mbvy, &ux, &uy);
+      A2 = edge_mask<true>(c, ux, uy);
+    }
+#endif
     bool done = ((A2 ^ act) & valid) == 0u;
     Contacts cn;
     uint32_t valid_n = 0u;
+#ifndef OGBX_PIPE_CHECK_FIRST
     if (more) valid_n = lean_slots(pm, L, k, cn);
+#endif
     OGBX_WSTAT(9, true);
     OGBX_WSTAT(13, !done);
     OGBX_WSTAT(10, band_next);
 #ifdef OGBX_ABL_PIPE_NOITER
     done = true;  // timing-only ablation: no active-set iteration (changes the physics)
+#endif
+#ifdef OGBX_PHYS_STATS
+    if (!done) {
+      const uint32_t chg = (A2 ^ act) & valid, fresh = valid & ~valid_prev;
+      OGBX_STAT(0);
+      if (chg & fresh) OGBX_STAT(1);
+      if (chg & ~fresh & 0xDBu) OGBX_STAT(2);
+      if (chg & ~fresh & 0x124u) OGBX_STAT(3);
+      if (st < 3) OGBX_STAT(6 + st);
+      if (e == 0) OGBX_STAT(21);
+      if (e == 0 && __builtin_popcount(valid) > 3) OGBX_STAT(22);
+      if (e == 4) OGBX_STAT(23);
+      if (e >= 1 && e <= 3) OGBX_STAT(23 + e);
+      if (e >= 5 && e <= 7) OGBX_STAT(22 + e);
+      if (e >= 8) OGBX_STAT(30);
+      // the largest |residual| among the edges whose activity flips
+      double rmax = 0.0;
+      const ContactSlot* sl[3] = {&c.s0, &c.s1, &c.s2};
+      for (int q = 0; q < 3; ++q) {
+        double a, b;
+        slot_res<true>(c, q, ux, uy, &a, &b);
+        const double r[3] = {a + b, a - b, a};
+        for (int t = 0; t < 3; ++t)
+          if ((chg >> (3 * q + t)) & 1u) rmax = fmax(rmax, fabs(r[t]));
+      }
+      OGBX_STAT(rmax < 1e-12 ? 16 : (rmax < 1e-9 ? 17 : (rmax < 1e-6 ? 18 : (rmax < 1e-3 ? 19 : 20))));
+    }
+    int trips = 0;
 #endif
     if (__builtin_expect(__any(!done | band_next), 0)) {
       OGBX_WPATH(0);
@@ -722,6 +769,10 @@ __device__ __forceinline__ void contact_loop_pipe(const PointModel& pm, double& 
 #pragma unroll 1
         for (int it = 0; it < OGBX_LEAN_ITERS && !done; ++it) {
           OGBX_WPATH(20);
+#ifdef OGBX_PHYS_STATS
+          OGBX_STAT(4);
+          ++trips;
+#endif
           act = A2 & valid;
           piece_weights(act, pw);
           piece_min<true>(pm, c, pw, mbvx, mbvy, &ux, &uy);
@@ -729,9 +780,20 @@ __device__ __forceinline__ void contact_loop_pipe(const PointModel& pm, double& 
           done = ((A2 ^ act) & valid) == 0u;
         }
         bl |= !done;
+#ifdef OGBX_PHYS_STATS
+        if (trips == 1) OGBX_STAT(5);
+#endif
       }
+#ifndef OGBX_PIPE_CHECK_FIRST
       if (more && __any(band_next)) lean_band(pm, k, cn);
+#endif
     }
+#ifdef OGBX_PIPE_CHECK_FIRST
+    if (more) {
+      lean_collide(pm, L, nqx, nqy, k, emin, emax);
+      valid_n = lean_slots(pm, L, k, cn);
+    }
+#endif
     double fx, fy;
     {
 #pragma clang fp contract(fast)
@@ -757,6 +819,9 @@ __device__ __forceinline__ void contact_loop_pipe(const PointModel& pm, double& 
       }
     }
     if (more) {
+#ifdef OGBX_PHYS_STATS
+      valid_prev = valid;
+#endif
       c = cn;
       valid = valid_n;
     }
@@ -769,6 +834,211 @@ __device__ __forceinline__ void contact_loop_pipe(const PointModel& pm, double& 
     if (w < 4096 && (int)(threadIdx.x & 63) == __ffsll((long long)b) - 1) g_wave_paths[w] = g_wpath;
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// The pipelined lean loop in the step's LOCAL frame (default; -DOGBX_LEAN_GLOBAL
+// restores contact_loop_pipe).  With the role sides fixed for the step
+// (lean_sides), reflect both axes so that they point at the step's walls:
+// X = sx (x - cx), Y = sy (y - cy) (exact: |x - cx| <= h and cx a multiple of
+// the unit, Sterbenz), velocities and accelerations likewise.  Then the face
+// normals are the constants (-1, 0) and (0, -1), the corner normal is
+// -(ex, ey) / |e| with ex = h - X, and t = perp(n) in the local frame (the
+// edge pair n +- t is symmetric under t -> -t, so the reflection needs no
+// relabelling of the mask; the first stage's mask, taken at u = 0, is
+// symmetric in the pair anyway).  Every per-stage multiplication by a side
+// sign disappears, and the face residuals become differences against
+// P = UX + UY, Q = UX - UY.  The position returns to the global frame once,
+// x = cx + sx X, at the end of the step.
+struct LocalSlots {
+  double kp0, kp1, kp2, w0, w1, w2, nx2, ny2;
+};
+
+// Normal-equation solve of the piece with weights p (local role layout).
+__device__ __forceinline__ void local_piece_min(const PointModel& pm, const LocalSlots& c, const PieceWeights& p,
+                                                double mbvx, double mbvy, double* ux, double* uy) {
+#pragma clang fp contract(fast)
+  const double M = pm.M;
+  const double w0 = c.w0, w1 = c.w1, w2 = c.w2;
+  double h00 = M + w0 * p.S0 + w1 * p.T1;
+  double h11 = M + w0 * p.T0 + w1 * p.S1;
+  double h01 = w0 * p.D0 - w1 * p.D1;
+  const double g0 = w0 * c.kp0, g1 = w1 * c.kp1;
+  double r0 = mbvx + g0 * p.S0 - g1 * p.D1;
+  double r1 = mbvy + g0 * p.D0 + g1 * p.S1;
+  const double nx = c.nx2, ny = c.ny2;
+  const double q = nx * nx, s = ny * ny, o = nx * ny;
+  const double WS = w2 * p.S2, WT = w2 * p.T2, WD = w2 * p.D2;
+  h00 += WS * q + WT * s - 2.0 * (WD * o);
+  h11 += WS * s + WT * q + 2.0 * (WD * o);
+  h01 += (WS - WT) * o + WD * (q - s);
+  const double k2 = c.kp2;
+  r0 -= k2 * (WS * nx - WD * ny);
+  r1 -= k2 * (WS * ny + WD * nx);
+  const double idet = fast_recip(h00 * h11 - h01 * h01);
+  *ux = (h11 * r0 - h01 * r1) * idet;
+  *uy = (h00 * r1 - h01 * r0) * idet;
+}
+
+// Active-edge mask at U (local role layout, bits as edge_mask).
+__device__ __forceinline__ uint32_t local_edge_mask(const LocalSlots& c, double ux, double uy) {
+#pragma clang fp contract(fast)
+  const double P = ux + uy, Q = ux - uy;
+  uint32_t m = (c.kp0 < P ? 1u : 0u) | (c.kp0 < Q ? 2u : 0u) | (c.kp0 < ux ? 4u : 0u);
+  m |= (c.kp1 < -Q ? 8u : 0u) | (c.kp1 < P ? 16u : 0u) | (c.kp1 < uy ? 32u : 0u);
+  const double a = c.nx2 * ux + (c.ny2 * uy + c.kp2);
+  const double b = c.nx2 * uy - c.ny2 * ux;
+  m |= (a < -b ? 64u : 0u) | (a < b ? 128u : 0u) | (a < 0.0 ? 256u : 0u);
+  return m;
+}
+
+__device__ __forceinline__ uint32_t local_slots(const PointModel& pm, const LeanSides& L, const LeanHit& k,
+                                                LocalSlots& c) {
+  c.nx2 = -(k.ex * k.inv);
+  c.ny2 = -(k.ey * k.inv);
+  const double u0 = band_u(pm, k.d0), u1 = band_u(pm, k.d1), u2 = band_u(pm, k.d2);
+  const double p01 = u0 * u1, p = p01 * u2;
+  double r = __builtin_amdgcn_rcp(p);
+  r = fma(r, fma(-p, r, 1.0), r);
+  r = fma(r, fma(-p, r, 1.0), r);
+  const double r01 = r * u2;
+  const double idg = 1.0 / pm.diag;
+  c.w0 = k.cX ? fma(r01 * u1, idg, -idg) : 0.0;
+  c.w1 = k.cY ? fma(r01 * u0, idg, -idg) : 0.0;
+  c.w2 = k.cD ? fma(r * p01, idg, -idg) : 0.0;
+  c.kp0 = fma(-u0, pm.K, pm.K) * k.d0;
+  c.kp1 = fma(-u1, pm.K, pm.K) * k.d1;
+  c.kp2 = fma(-u2, pm.K, pm.K) * k.d2;
+  return (k.cX ? L.bX : 0u) | (k.cY ? L.bY : 0u) | (k.cD ? L.bD : 0u);
+}
+
+// Slot distances at the local position (X, Y) (lean_collide in the local frame).
+__device__ __forceinline__ void local_collide(const PointModel& pm, const LeanSides& L, double X, double Y,
+                                              LeanHit& k, double& emin, double& emax) {
+  const double hx = pm.box_hxy;
+  k.ex = hx - X;
+  k.ey = hx - Y;
+  emin = fmin(emin, fmin(k.ex, k.ey));
+  emax = fmax(emax, fmax(k.ex, k.ey));
+  k.d0 = k.ex - L.rX;
+  k.d1 = k.ey - L.rY;
+  const double d2 = fma(k.ex, k.ex, k.ey * k.ey);
+  k.cX = k.d0 <= 0.0;
+  k.cY = k.d1 <= 0.0;
+  k.cD = !(d2 > L.farD2);
+  const double y0 = __builtin_amdgcn_rsq(d2);
+  k.inv = y0 * fma(-0.5 * d2 * y0, y0, 1.5);
+  k.d2 = d2 * k.inv - L.rD;
+  k.band = false;
+}
+
+__device__ __forceinline__ void contact_loop_local(const PointModel& pm, double& x, double& y, const RoleFrame& fr,
+                                                   const Contacts& c0, uint32_t valid, bool* bail) {
+  bool bl = false;
+  const double h = pm.h;
+  const LeanSides L = lean_sides(pm, fr, x, y);
+  double emin = pm.box_hxy, emax = pm.box_hxy;
+  // local state: position, substep velocity, stage velocity, RK sums
+  double X = L.sxd * (x - L.cx), Y = L.syd * (y - L.cy);
+  double vx = 0.0, vy = 0.0, vsx = 0.0, vsy = 0.0;
+  double sqx = 0.0, sqy = 0.0, svx = 0.0, svy = 0.0;
+  // the first stage's exact contacts (stage_contacts), in the local frame
+  LocalSlots c;
+  c.kp0 = c0.s0.kp;
+  c.kp1 = c0.s1.kp;
+  c.kp2 = c0.s2.kp;
+  c.w0 = c0.s0.w;
+  c.w1 = c0.s1.w;
+  c.w2 = c0.s2.w;
+  c.nx2 = L.sxd * c0.s2.nx;
+  c.ny2 = L.syd * c0.s2.ny;
+  uint32_t act = local_edge_mask(c, 0.0, 0.0) & valid;
+  PieceWeights pw;
+  piece_weights(act, pw);
+  const double mB = pm.mass * pm.B;
+  const int nstage = 4 * pm.nsub;
+#pragma unroll OGBX_AS_UNROLL
+  for (int e = 0; e < nstage; ++e) {
+    const int st = e & 3;
+    const bool more = e + 1 < nstage;
+    double nqx, nqy, nsqx, nsqy, nx_ = X, ny_ = Y;
+    {
+#pragma clang fp contract(fast)
+      const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
+      nsqx = sqx + b * vsx;
+      nsqy = sqy + b * vsy;
+      if (st < 3) {
+        const double cf = (st < 2) ? 0.5 : 1.0;
+        nqx = X + h * (cf * vsx);
+        nqy = Y + h * (cf * vsy);
+      } else {
+        nx_ = X + h * nsqx;
+        ny_ = Y + h * nsqy;
+        nqx = nx_;
+        nqy = ny_;
+      }
+    }
+    LeanHit k;
+    if (more) local_collide(pm, L, nqx, nqy, k, emin, emax);
+    double ux, uy;
+    const double mbvx = mB * vsx, mbvy = mB * vsy;
+    local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+    uint32_t A2 = local_edge_mask(c, ux, uy);
+#ifndef OGBX_NO_FIRST_TRIP
+    if (e == 0) {  // see contact_loop_pipe
+      act = A2 & valid;
+      piece_weights(act, pw);
+      local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+      A2 = local_edge_mask(c, ux, uy);
+    }
+#endif
+    bool done = ((A2 ^ act) & valid) == 0u;
+    LocalSlots cn;
+    uint32_t valid_n = 0u;
+    if (more) valid_n = local_slots(pm, L, k, cn);
+    if (__builtin_expect(__any(!done), 0)) {
+#pragma unroll 1
+      for (int it = 0; it < OGBX_LEAN_ITERS && !done; ++it) {
+        act = A2 & valid;
+        piece_weights(act, pw);
+        local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+        A2 = local_edge_mask(c, ux, uy);
+        done = ((A2 ^ act) & valid) == 0u;
+      }
+      bl |= !done;
+    }
+    double fx, fy;
+    {
+#pragma clang fp contract(fast)
+      fx = ux - pm.B * vsx;
+      fy = uy - pm.B * vsy;
+      const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
+      svx = svx + b * fx;
+      svy = svy + b * fy;
+      if (st < 3) {
+        const double cf = (st < 2) ? 0.5 : 1.0;
+        sqx = nsqx;
+        sqy = nsqy;
+        vsx = vx + (cf * fx) * h;
+        vsy = vy + (cf * fy) * h;
+      } else {
+        vx = vx + svx * h;
+        vy = vy + svy * h;
+        X = nx_;
+        Y = ny_;
+        vsx = vx;
+        vsy = vy;
+        sqx = sqy = svx = svy = 0.0;
+      }
+    }
+    if (more) {
+      c = cn;
+      valid = valid_n;
+    }
+  }
+  *bail = bl | !(emin > 0.0) | !(emax < pm.box_hxy + 1.25);
+  x = fma(L.sxd, X, L.cx);
+  y = fma(L.syd, Y, L.cy);
 }
 
 // One PointEnv physics step (same RK4 loop as point_physics.h point_step).
@@ -792,8 +1062,10 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
   const double x0 = x, y0 = y;
 #ifndef OGBX_NO_LEAN_SPLIT
   bool bail = true;
-#ifndef OGBX_LEAN_SERIAL
+#if defined(OGBX_LEAN_GLOBAL)
   if (!__any(generic)) contact_loop_pipe(pm, x, y, fr, c, valid, &bail);
+#elif !defined(OGBX_LEAN_SERIAL)
+  if (!__any(generic)) contact_loop_local(pm, x, y, fr, c, valid, &bail);
 #else
   if (!__any(generic)) contact_loop<true>(pm, wall, H, W, x, y, fr, c, valid, false, &bail);
 #endif

@@ -120,7 +120,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 #ifdef OGBX_PHYS_STATS
 // Diagnostic build only (-DOGBX_PHYS_STATS): per-path counters.
-__device__ unsigned long long g_phys_stats[16];
+__device__ unsigned long long g_phys_stats[32];
 #define OGBX_STAT(k) atomicAdd(&g_phys_stats[k], 1ull)
 // once per wave when any active lane satisfies cond
 #define OGBX_WSTAT(k, cond) do {                                                   \

@@ -10,7 +10,7 @@ from ogbench_amd import _lib
 from oracle import locomaze as orc
 dev = torch.device('cuda', 0)
 L = _lib.lib()
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 32)()
 L.ogbx_diag_phys_stats(buf)
 for maze in ('medium', 'large', 'giant', 'arena'):
     rng = np.random.RandomState(sum(map(ord, maze)))
@@ -38,3 +38,9 @@ L.ogbx_diag_phys_stats(buf)
 s = list(buf)
 print(f'bench 300 steps: contact wave-stages {s[9]} bail waves {s[14]} slow wave-stages {s[12]} '
       f'iterating wave-stages {s[13]} band wave-stages {s[10]}', flush=True)
+print(f'  lanes iterating {s[0]}: new contact {s[1]}, friction edge {s[2]}, normal edge {s[3]}; '
+      f'trips {s[4]}, settled in one trip {s[5]}; by RK stage 0/1/2: {s[6]} {s[7]} {s[8]}', flush=True)
+print(f'  flipping-edge |residual| max: <1e-12 {s[16]}, <1e-9 {s[17]}, <1e-6 {s[18]}, <1e-3 {s[19]}, larger {s[20]}',
+      flush=True)
+print(f'  first stage of the step {s[21]} (with >= 2 contacts {s[22]}), stage 4 {s[23]}', flush=True)
+print(f'  by stage e = 1, 2, 3: {s[24]} {s[25]} {s[26]}; e = 5, 6, 7: {s[27]} {s[28]} {s[29]}; e >= 8: {s[30]}', flush=True)

@@ -22,7 +22,7 @@ for spread in [0.5, 1.3, 1.9]:
     out, cf = env.physics(q, a)
     torch.cuda.synchronize()
     if stats:
-        buf = (ctypes.c_ulonglong * 16)()
+        buf = (ctypes.c_ulonglong * 32)()
         stats(buf)
     evs = []
     for _ in range(30):
@@ -32,7 +32,7 @@ for spread in [0.5, 1.3, 1.9]:
     ms = np.median([s.elapsed_time(e) for s, e in evs])
     line = f'{tag} spread {spread}: contact {cf.float().mean().item():.3f} kernel {ms*1e3:.1f} us'
     if stats:
-        buf = (ctypes.c_ulonglong * 16)()
+        buf = (ctypes.c_ulonglong * 32)()
         env.physics(q, a); torch.cuda.synchronize(); stats(buf)
         line += f' | stages n0..3={list(buf)[:4]} newton_its={buf[4]} fallbacks={buf[5]} slowpaths={buf[6]}'
     print(line, flush=True)

@@ -11,7 +11,7 @@ n = 65536
 env = ogbench_amd.make('pointmaze-large-v0', num_envs=n, device=dev, auto_reset=True)
 L = _lib.lib()
 stats = hasattr(L, 'ogbx_diag_phys_stats')
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 32)()
 env.reset(seed=0, options=dict(task_id=(torch.arange(n, device=dev, dtype=torch.int32) % 5) + 1))
 g = torch.Generator(device=dev); g.manual_seed(1)
 acts = torch.rand(64, n, 2, device=dev, generator=g) * 2 - 1

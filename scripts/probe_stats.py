@@ -18,7 +18,7 @@ acts = torch.rand(64, n, 2, device=dev) * 2 - 1
 for i in range(300):
     env.step(acts[i % 64])
 torch.cuda.synchronize()
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 32)()
 L.ogbx_diag_phys_stats(buf)
 for rep in range(3):
     env.step(acts[rep]); torch.cuda.synchronize()
