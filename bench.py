@@ -708,12 +708,14 @@ def bench_powder(args, world, rank, dev, level='easy'):
         nonlocal out
         out = env.rollout(fk_actions, out=out)
 
+    if full and not args.no_extras:
+        extra.update(_powder_phases(env, step, steps, dev))
     if not args.no_extras:
         fused(0)
         reps = max(1, steps // K)
         fdt = _timed(fused, reps, world, dev)
         fk_ms = _per_launch_ms(fused, 3, dev)
-        extra = dict(fused_k48_steps_per_s=n * K * reps * world / fdt, fused_k48_kernel_ms=fk_ms,
+        extra.update(fused_k48_steps_per_s=n * K * reps * world / fdt, fused_k48_kernel_ms=fk_ms,
                      fused_k48_achieved_GBs=per_step * n * K / (fk_ms * 1e-3) / 1e9)
     result = dict(
         metric=f'env steps/sec, powderworld-{level}-v0 64x64, N={n} parallel envs per GPU',
@@ -762,6 +764,48 @@ def cpu_baseline_powder(size, args):
     dt = time.perf_counter() - t0
     return dict(value=n / dt, unit='env_steps/s', cores=1, kind='port',
                 sample=f'{n} single-env steps of powderworld-easy {size}x{size} ({dt:.1f} s)')
+
+
+def _powder_phases(env, step, start, dev):
+    """Medium/hard: the steady-state step and the synchronized auto-reset step
+    priced apart (device time on the launch stream).  Every env starts its
+    episode together, so all of them auto-reset (goal replay) in the same step
+    every max_episode_steps steps (envs that reach their goal earlier reset on
+    their own, rarely under random actions).  Steady state: the mean of a
+    window of whole 3-step action cycles that contains no synchronized reset;
+    reset step: the one step in which the synchronized reset happens."""
+    el = int(env.state_dict()['elapsed'][0])
+    T = env.max_episode_steps
+    left = T - el  # the step with index start + left - 1 is the synchronized reset
+    i = start
+    stream = torch.cuda.current_stream(dev)
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    win = min(300, left - 1) // 3 * 3
+    out = {}
+    if win >= 3:
+        a, b = ev(), ev()
+        torch.cuda.synchronize(dev)
+        a.record(stream)
+        for _ in range(win):
+            step(i)
+            i += 1
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        out['steady_state_ms_per_step'] = a.elapsed_time(b) / win
+        out['steady_state_window_steps'] = win
+    while i < start + left - 1:  # up to the step before the reset
+        step(i)
+        i += 1
+    a, b = ev(), ev()
+    torch.cuda.synchronize(dev)
+    a.record(stream)
+    step(i)
+    b.record(stream)
+    torch.cuda.synchronize(dev)
+    out['sync_reset_step_ms'] = a.elapsed_time(b)
+    out['sync_reset_envs'] = int((env.state_dict()['elapsed'] == 0).sum())
+    out['sync_reset_every_steps'] = T
+    return out
 
 
 def cpu_baseline_powder_full(ne, size, args):
