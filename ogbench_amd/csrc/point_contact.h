@@ -932,8 +932,12 @@ __device__ __forceinline__ void local_collide(const PointModel& pm, const LeanSi
   k.band = false;
 }
 
+// c0 == nullptr: the first stage's slots come from the local collider too
+// (the default; the reported contact flag is computed separately with the
+// oracle's exact arithmetic, contact_flags); else from the exact
+// stage_contacts (-DOGBX_FIRST_EXACT_SLOTS).
 __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double& x, double& y, const RoleFrame& fr,
-                                                   const Contacts& c0, uint32_t valid, bool* bail) {
+                                                   const Contacts* c0, uint32_t valid, bool* bail) {
   bool bl = false;
   const double h = pm.h;
   const LeanSides L = lean_sides(pm, fr, x, y);
@@ -942,16 +946,22 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
   double X = L.sxd * (x - L.cx), Y = L.syd * (y - L.cy);
   double vx = 0.0, vy = 0.0, vsx = 0.0, vsy = 0.0;
   double sqx = 0.0, sqy = 0.0, svx = 0.0, svy = 0.0;
-  // the first stage's exact contacts (stage_contacts), in the local frame
   LocalSlots c;
-  c.kp0 = c0.s0.kp;
-  c.kp1 = c0.s1.kp;
-  c.kp2 = c0.s2.kp;
-  c.w0 = c0.s0.w;
-  c.w1 = c0.s1.w;
-  c.w2 = c0.s2.w;
-  c.nx2 = L.sxd * c0.s2.nx;
-  c.ny2 = L.syd * c0.s2.ny;
+  if (c0 == nullptr) {
+    LeanHit k0;
+    local_collide(pm, L, X, Y, k0, emin, emax);
+    valid = local_slots(pm, L, k0, c);
+  } else {
+    // the first stage's exact contacts (stage_contacts), in the local frame
+    c.kp0 = c0->s0.kp;
+    c.kp1 = c0->s1.kp;
+    c.kp2 = c0->s2.kp;
+    c.w0 = c0->s0.w;
+    c.w1 = c0->s1.w;
+    c.w2 = c0->s2.w;
+    c.nx2 = L.sxd * c0->s2.nx;
+    c.ny2 = L.syd * c0->s2.ny;
+  }
   uint32_t act = local_edge_mask(c, 0.0, 0.0) & valid;
   PieceWeights pw;
   piece_weights(act, pw);
@@ -1041,6 +1051,29 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
   y = fma(L.syd, Y, L.cy);
 }
 
+// The first stage's contact flag with collide_roles' exact arithmetic (the
+// reported flag and the free/contact split are bit-exact with the oracle), no
+// slot data.  *slow: the lane needs the generic collider.
+__device__ __forceinline__ uint32_t contact_flags(const PointModel& pm, const RoleFrame& f, double x, double y,
+                                                  bool* slow) {
+  const double lx = x - f.cx, ly = y - f.cy;
+  *slow = f.slow | !(fabs(lx) < pm.box_hxy) | !(fabs(ly) < pm.box_hxy);
+  const double reach = pm.box_hxy - pm.radius - 1e-9;
+  const int sx = lx >= reach ? 1 : (lx <= -reach ? -1 : 0);
+  const int sy = ly >= reach ? 1 : (ly <= -reach ? -1 : 0);
+  const double sxd = (double)sx, syd = (double)sy;
+  const double hx = pm.box_hxy, r = pm.radius;
+  const uint32_t vX = (f.m >> (4 + sx)) & 1u;
+  const uint32_t vY = (f.m >> (4 + 3 * sy)) & 1u;
+  const uint32_t vD = (f.m >> (4 + 3 * sy + sx)) & (uint32_t)(sx & sy) & 1u;
+  const double px = x - fma(sxd, pm.unit, f.cx), py = y - fma(syd, pm.unit, f.cy);
+  const double tx = fma(-sxd, hx, -px), ty = fma(-syd, hx, -py);
+  const bool cX = vX & (fabs(tx) - r <= 0.0);
+  const bool cY = vY & (fabs(ty) - r <= 0.0);
+  const bool cD = vD & !(tx * tx + ty * ty > kPointFarD2);
+  return (cX ? kSlotBits : 0u) | (cY ? kSlotBits << 3 : 0u) | (cD ? kSlotBits << 6 : 0u);
+}
+
 // One PointEnv physics step (same RK4 loop as point_physics.h point_step).
 __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_t* wall, int H, int W,
                                              double* px, double* py) {
@@ -1048,6 +1081,41 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
   Contacts c;
   RoleFrame fr;
   role_frame(pm, wall, H, W, x, y, fr);
+#if !defined(OGBX_LEAN_GLOBAL) && !defined(OGBX_LEAN_SERIAL) && !defined(OGBX_NO_LEAN_SPLIT) && \
+    !defined(OGBX_FIRST_EXACT_SLOTS)
+  {
+    // exact first-stage flags; the lean loop computes its own first-stage
+    // slots; the full loop (one call site) takes waves with a generic lane
+    // and lanes that bail
+    bool slow;
+    const uint32_t v1 = contact_flags(pm, fr, x, y, &slow);
+    bool in_contact = v1 != 0, bail = true;
+    const bool any_slow = __any(slow);
+    if (any_slow) {
+      bool generic;
+      in_contact = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic) != 0;
+    }
+    if (!__any(in_contact)) {
+      *px = x + 0.0;
+      *py = y + 0.0;
+      return 0;
+    }
+    const double x0 = x, y0 = y;
+    if (!any_slow) contact_loop_local(pm, x, y, fr, nullptr, 0u, &bail);
+    OGBX_WSTAT(14, bail);
+    if (__builtin_expect(__any(bail), 0)) {
+      x = x0;
+      y = y0;
+      role_frame(pm, wall, H, W, x, y, fr);
+      bool generic;
+      const uint32_t valid = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic);
+      contact_loop<false>(pm, wall, H, W, x, y, fr, c, valid, generic, &bail);
+    }
+    *px = in_contact ? x : x0 + 0.0;
+    *py = in_contact ? y : y0 + 0.0;
+    return in_contact ? 1 : 0;
+  }
+#else
   bool generic;
   uint32_t valid = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic);
   const bool in_contact = valid != 0;
@@ -1065,7 +1133,9 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
 #if defined(OGBX_LEAN_GLOBAL)
   if (!__any(generic)) contact_loop_pipe(pm, x, y, fr, c, valid, &bail);
 #elif !defined(OGBX_LEAN_SERIAL)
-  if (!__any(generic)) contact_loop_local(pm, x, y, fr, c, valid, &bail);
+#ifdef OGBX_FIRST_EXACT_SLOTS
+  if (!__any(generic)) contact_loop_local(pm, x, y, fr, &c, valid, &bail);
+#endif
 #else
   if (!__any(generic)) contact_loop<true>(pm, wall, H, W, x, y, fr, c, valid, false, &bail);
 #endif
@@ -1085,6 +1155,7 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
   *px = in_contact ? x : x0 + 0.0;
   *py = in_contact ? y : y0 + 0.0;
   return in_contact ? 1 : 0;
+#endif
 }
 
 }  // namespace ogbx
