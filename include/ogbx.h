@@ -76,12 +76,11 @@ typedef struct {
                                 G ranks holding envs [r*N/G, (r+1)*N/G) with one
                                 shared seed reproduce the single-GPU run of N
                                 envs bit for bit.  0 = unsharded.
-                                Shard boundaries must be multiples of 64 envs:
-                                the contact solver's wave-uniform path choices
-                                depend on which 64 envs share a wavefront, so a
-                                boundary inside a wave changes results at the
-                                rounding level (ogbench_amd.sharding.shard
-                                enforces this). */
+                                Any boundary works: every contact-solver choice
+                                is made per env, so results do not depend on
+                                which envs share a wavefront (multiples of 64
+                                envs keep the wavefronts full;
+                                ogbench_amd.sharding.shard aligns to 64). */
 } ogbx_maze_opts;
 
 /* Create a batch of `n_envs` maze envs on `device`.

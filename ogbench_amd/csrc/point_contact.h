@@ -351,25 +351,30 @@ __device__ __forceinline__ void solve_active_set(const PointModel& pm, const Con
   *uy_out = uy;
 }
 
-// Contacts at a stage: the role collider, or (wave-uniform, rare) the generic
-// collider for the lanes whose frame is slow, whose slots then hold contacts
-// 0..n-1 with explicit tangents (empty slots zero rows).  Returns the
-// validity mask; *generic tells which evaluation the wave uses.
+// Contacts at a stage: the role collider, or (rare) the generic collider for
+// the lanes whose frame is slow, whose slots then hold contacts 0..n-1 with
+// explicit tangents (empty slots zero rows).  Returns the validity mask;
+// *generic tells which evaluation THIS LANE uses: the choice is per lane (the
+// wave runs both evaluations when it holds both kinds), so a lane's result
+// never depends on which envs share its wavefront.
 __device__ __forceinline__ uint32_t stage_contacts(const PointModel& pm, const uint16_t* wall, int H, int W,
                                                    double x, double y, const RoleFrame& fr, Contacts& c,
                                                    bool* generic) {
   bool slow;
   uint32_t valid = collide_roles(pm, fr, x, y, c, &slow);
-  *generic = false;
+  *generic = slow;
   OGBX_WSTAT(12, slow);
 #ifndef OGBX_ABL_NOSLOW
   if (__builtin_expect(__any(slow), 0)) {
 #else
   if (false) {
 #endif
+#ifdef OGBX_WAVE_BAIL  // A/B: the round-2 wave-level choice
     *generic = true;
     role_tangents(c);
+#endif
     if (slow) {
+      role_tangents(c);
       const double lx = x - fr.cx, ly = y - fr.cy;
       const double reach = pm.box_hxy - pm.radius - 1e-9;
       const int sx = lx >= reach ? 1 : (lx <= -reach ? -1 : 0);
@@ -854,9 +859,16 @@ struct LocalSlots {
   double kp0, kp1, kp2, w0, w1, w2, nx2, ny2;
 };
 
+// The 2x2 normal matrix of the last solve and its inverse determinant (for
+// the rank-one update of a single flipped edge).
+struct PieceSys {
+  double h00, h01, h11, idet;
+};
+
 // Normal-equation solve of the piece with weights p (local role layout).
 __device__ __forceinline__ void local_piece_min(const PointModel& pm, const LocalSlots& c, const PieceWeights& p,
-                                                double mbvx, double mbvy, double* ux, double* uy) {
+                                                double mbvx, double mbvy, double* ux, double* uy,
+                                                PieceSys* sys = nullptr) {
 #pragma clang fp contract(fast)
   const double M = pm.M;
   const double w0 = c.w0, w1 = c.w1, w2 = c.w2;
@@ -878,6 +890,35 @@ __device__ __forceinline__ void local_piece_min(const PointModel& pm, const Loca
   const double idet = fast_recip(h00 * h11 - h01 * h01);
   *ux = (h11 * r0 - h01 * r1) * idet;
   *uy = (h00 * r1 - h01 * r0) * idet;
+  if (sys) *sys = PieceSys{h00, h01, h11, idet};
+}
+
+// The solve of the piece that differs from the solved one (system S, solution
+// u) by the single edge `e` (bit index): adding (delta = +1) or removing (-1)
+// edge e changes the normal equations by the rank-one term delta c w J J' on
+// the left and -delta c w kp J on the right, so by Sherman-Morrison
+//   u' = u - a rho H^-1 J / (1 + a J' H^-1 J),  a = delta c w,  rho = J.u + kp
+// (rho: the edge's residual at u).  ~30 instructions instead of rebuilding the
+// piece.  Removing an edge keeps H' = M I + (the other edges) positive
+// definite, so the denominator stays positive.
+__device__ __forceinline__ void local_rank_one(const LocalSlots& c, const PieceSys& S, uint32_t act, int e,
+                                               double* ux, double* uy) {
+#pragma clang fp contract(fast)
+  const int s = e >= 6 ? 2 : (e >= 3 ? 1 : 0), t = e - 3 * s;
+  // slot selection as 0/1 weights, not selects: LLVM turns a select chain over
+  // the slot fields into a stack array indexed by s (scratch stores per stage)
+  const double f0 = (double)(s == 0), f1 = (double)(s == 1), f2 = (double)(s == 2);
+  const double nx = f2 * c.nx2 - f0, ny = f2 * c.ny2 - f1;
+  const double sg = (double)(t == 0) - (double)(t == 1);
+  const double jx = nx - sg * ny, jy = ny + sg * nx;  // n + sg t, t = (-ny, nx)
+  const double w = f0 * c.w0 + f1 * c.w1 + f2 * c.w2;
+  const double kp = f0 * c.kp0 + f1 * c.kp1 + f2 * c.kp2;
+  const double a = (((act >> e) & 1u) ? -1.0 : 1.0) * (t == 2 ? 2.0 * w : w);
+  const double rho = jx * *ux + (jy * *uy + kp);
+  const double zx = (S.h11 * jx - S.h01 * jy) * S.idet, zy = (S.h00 * jy - S.h01 * jx) * S.idet;
+  const double f = a * rho * fast_recip(1.0 + a * (jx * zx + jy * zy));
+  *ux -= f * zx;
+  *uy -= f * zy;
 }
 
 // Active-edge mask at U (local role layout, bits as edge_mask).
@@ -992,13 +1033,14 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
     if (more) local_collide(pm, L, nqx, nqy, k, emin, emax);
     double ux, uy;
     const double mbvx = mB * vsx, mbvy = mB * vsy;
-    local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+    PieceSys sys;
+    local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy, &sys);
     uint32_t A2 = local_edge_mask(c, ux, uy);
 #ifndef OGBX_NO_FIRST_TRIP
     if (e == 0) {  // see contact_loop_pipe
       act = A2 & valid;
       piece_weights(act, pw);
-      local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+      local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy, &sys);
       A2 = local_edge_mask(c, ux, uy);
     }
 #endif
@@ -1006,9 +1048,36 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
     LocalSlots cn;
     uint32_t valid_n = 0u;
     if (more) valid_n = local_slots(pm, L, k, cn);
+#ifdef OGBX_PHYS_STATS
+    if (!done) {
+      const int pc = __builtin_popcount((A2 ^ act) & valid);
+      OGBX_STAT(0);
+      OGBX_STAT(pc == 1 ? 1 : (pc == 2 ? 2 : 3));
+    }
+    int trips = 0;
+#endif
     if (__builtin_expect(__any(!done), 0)) {
+#ifdef OGBX_RANK_ONE
+      // 99 % of the lanes that iterate flip exactly one edge (counters,
+      // scripts/probe_bail.py): their next piece is a rank-one update.
+      // Opt-in (-DOGBX_RANK_ONE): measured slower on gfx950 (13.75 vs 13.2 us
+      // at N = 65,536) -- the hot stage keeps the 2x2 system live for it and
+      // the cold block grows; the rebuilt piece costs little more.
+      const uint32_t chg = (A2 ^ act) & valid;
+      if (!done && (chg & (chg - 1u)) == 0u) {
+        local_rank_one(c, sys, act, __builtin_ctz(chg), &ux, &uy);
+        act ^= chg;
+        A2 = local_edge_mask(c, ux, uy);
+        done = ((A2 ^ act) & valid) == 0u;
+      }
+      if (__any(!done)) {
+#endif
 #pragma unroll 1
       for (int it = 0; it < OGBX_LEAN_ITERS && !done; ++it) {
+#ifdef OGBX_PHYS_STATS
+        OGBX_STAT(4);
+        ++trips;
+#endif
         act = A2 & valid;
         piece_weights(act, pw);
         local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
@@ -1016,6 +1085,13 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
         done = ((A2 ^ act) & valid) == 0u;
       }
       bl |= !done;
+#ifdef OGBX_PHYS_STATS
+      if (trips == 1) OGBX_STAT(5);
+#endif
+#ifdef OGBX_RANK_ONE
+      }
+      piece_weights(act, pw);  // the next stage's warm start
+#endif
     }
     double fx, fy;
     {
@@ -1087,11 +1163,42 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
     // exact first-stage flags; the lean loop computes its own first-stage
     // slots; the full loop (one call site) takes waves with a generic lane
     // and lanes that bail
+    // Every choice is per lane, so a lane's result never depends on which envs
+    // share its wavefront (any sharding of the envs reproduces the single
+    // run): the lean loop's result is kept unless THIS lane bails or needs the
+    // generic collider, in which case the full loop's result is taken.
     bool slow;
     const uint32_t v1 = contact_flags(pm, fr, x, y, &slow);
-    bool in_contact = v1 != 0, bail = true;
-    const bool any_slow = __any(slow);
-    if (any_slow) {
+    bool in_contact = v1 != 0;
+#ifdef OGBX_WAVE_BAIL
+    {
+      bool bail = true;
+      const bool any_slow = __any(slow);
+      if (any_slow) {
+        bool generic;
+        in_contact = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic) != 0;
+      }
+      if (!__any(in_contact)) {
+        *px = x + 0.0;
+        *py = y + 0.0;
+        return 0;
+      }
+      const double x0 = x, y0 = y;
+      if (!any_slow) contact_loop_local(pm, x, y, fr, nullptr, 0u, &bail);
+      if (__builtin_expect(__any(bail), 0)) {
+        x = x0;
+        y = y0;
+        role_frame(pm, wall, H, W, x, y, fr);
+        bool generic;
+        const uint32_t valid = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic);
+        contact_loop<false>(pm, wall, H, W, x, y, fr, c, valid, generic, &bail);
+      }
+      *px = in_contact ? x : x0 + 0.0;
+      *py = in_contact ? y : y0 + 0.0;
+      return in_contact ? 1 : 0;
+    }
+#endif
+    if (__builtin_expect(__any(slow), 0)) {
       bool generic;
       in_contact = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic) != 0;
     }
@@ -1101,15 +1208,18 @@ __device__ __forceinline__ int point_step_as(const PointModel& pm, const uint16_
       return 0;
     }
     const double x0 = x, y0 = y;
-    if (!any_slow) contact_loop_local(pm, x, y, fr, nullptr, 0u, &bail);
+    bool bail;
+    contact_loop_local(pm, x, y, fr, nullptr, 0u, &bail);  // a slow lane's values are discarded
+    bail |= slow;
     OGBX_WSTAT(14, bail);
     if (__builtin_expect(__any(bail), 0)) {
-      x = x0;
-      y = y0;
-      role_frame(pm, wall, H, W, x, y, fr);
-      bool generic;
-      const uint32_t valid = stage_contacts(pm, wall, H, W, x, y, fr, c, &generic);
-      contact_loop<false>(pm, wall, H, W, x, y, fr, c, valid, generic, &bail);
+      double xf = x0, yf = y0;
+      role_frame(pm, wall, H, W, xf, yf, fr);
+      bool generic, b2;
+      const uint32_t valid = stage_contacts(pm, wall, H, W, xf, yf, fr, c, &generic);
+      contact_loop<false>(pm, wall, H, W, xf, yf, fr, c, valid, generic, &b2);
+      x = bail ? xf : x;
+      y = bail ? yf : y;
     }
     *px = in_contact ? x : x0 + 0.0;
     *py = in_contact ? y : y0 + 0.0;

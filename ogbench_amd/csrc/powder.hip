@@ -653,6 +653,13 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
 
 // k_steps env steps; rand: [k, N, 3, H, W] injected fields for the forward of
 // each third step, or NULL = Philox (auto-resets always use Philox).
+#ifdef OGBX_PWF_STAMPS
+// Diagnostic build only: per-env wall clock (s_memrealtime, 100 MHz) at entry,
+// after the state load, before the observation and at exit of the last
+// pwf_step_kernel launch.
+__device__ unsigned long long g_pwf_stamps[4096 * 4];
+#endif
+
 template <int WS>
 __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(OGBX_PWF_WAVES))) pwf_step_kernel(
     const PowderParams* __restrict__ Pp, PowderState S, int64_t n, const int32_t* __restrict__ action,
@@ -669,6 +676,9 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   pwf_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
   const int max_steps = Pp->max_steps;
+#ifdef OGBX_PWF_STAMPS
+  const unsigned long long ts0 = wall_clock64();
+#endif
   fw.load(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) sh.g[fw.cell(k)] = S.goal_env[(size_t)e * C + fw.cell(k)];
@@ -679,6 +689,10 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   const int tol = Pp->tol_task[(task >= 1 && task <= Pp->num_tasks ? task : 1) - 1];
   bool dirty = false, goal_dirty = false;
   __syncthreads();
+#ifdef OGBX_PWF_STAMPS
+  const unsigned long long ts1 = wall_clock64();
+  unsigned long long ts2 = ts1;
+#endif
   const int len = Pp->seq_len[task - 1];
   for (int k = 0; k < k_steps; ++k) {
     fw.fence_idx();
@@ -744,9 +758,21 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     }
     ctrl = stage | (elem << 2) | (x << 8) | (ctrl & (255 << 16)) | (succ ? kCtrlSuccess : 0);
     const uint32_t acol = sh.lut[sh.elem_ids[elem & 7] & 31];
+#ifdef OGBX_PWF_STAMPS
+    ts2 = wall_clock64();
+#endif
     fw.observe(obs + (size_t)o * C * 6, stage, acol, x * grid, brush);
   }
   if (dirty) fw.store(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
+#ifdef OGBX_PWF_STAMPS
+  if (threadIdx.x == 0 && e < 4096) {
+    const unsigned long long ts3 = wall_clock64();
+    g_pwf_stamps[4 * e + 0] = ts0;
+    g_pwf_stamps[4 * e + 1] = ts1;
+    g_pwf_stamps[4 * e + 2] = ts2;
+    g_pwf_stamps[4 * e + 3] = ts3;
+  }
+#endif
   if (goal_dirty) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
@@ -1107,6 +1133,14 @@ ogbx_status ogbx_powder_task_table(int32_t num_elems, int32_t task_id, int32_t* 
       for (int k = 0; k < 3; ++k) seq[3 * q + k] = t[q][k];
   return OGBX_OK;
 }
+
+#ifdef OGBX_PWF_STAMPS
+extern "C" ogbx_status ogbx_diag_pwf_stamps(unsigned long long* out) {
+  OGBX_HIP(hipDeviceSynchronize());
+  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(ogbx::g_pwf_stamps), 4096 * 4 * sizeof(unsigned long long)));
+  return OGBX_OK;
+}
+#endif
 
 ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int32_t device,
                                ogbx_powder_t* out) {

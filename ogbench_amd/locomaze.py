@@ -90,9 +90,9 @@ class MazeEnv:
         """env_base: global index of env 0 of this batch.  Every Philox stream
         is counted by the global env index, so G shards [r*N/G, (r+1)*N/G) with
         the same seed reproduce one batch of N envs bit for bit.
-        Shard boundaries must be multiples of 64 envs (the contact solver's
-        wave-uniform choices depend on which envs share a wavefront); use
-        ogbench_amd.sharding.shard."""
+        Any boundary works (every contact-solver choice is made per env, so
+        results do not depend on which envs share a wavefront);
+        ogbench_amd.sharding.shard keeps blocks 64-aligned for full wavefronts."""
         if loco_env_type not in LOCO_TYPES:
             raise ValueError(f'Unknown locomotion environment type: {loco_env_type}')
         if maze_type not in MAZE_TYPES:

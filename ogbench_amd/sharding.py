@@ -9,9 +9,11 @@ single-GPU job of the same ``total`` bit for bit.  There is no per-step
 exchange; the only collective is the eval all-gather
 (``evaluation.gather_counters``).
 
-Bit-identity also needs the same lane grouping on every rank: the maze step
-kernel picks some solver paths per 64-lane wave, so shard sizes are kept
-multiples of 64 envs (``align``).
+Bit-identity does not depend on how envs are grouped into wavefronts: every
+contact-solver choice of the maze step is made per lane (round 3,
+``tests/test_locomaze_gpu.py::test_results_do_not_depend_on_wavefront_composition``).
+Blocks are still kept multiples of 64 envs (``align``) so that every rank's
+wavefronts are full.
 """
 
 from __future__ import annotations
@@ -21,7 +23,7 @@ def shard(total, world, rank, align=64):
     """(env_base, num_envs) of `rank` for `total` envs over `world` ranks.
 
     Blocks are contiguous and, except possibly the last, multiples of `align`
-    envs, so that wave-level solver choices group the same envs on every rank.
+    envs (full 64-lane wavefronts; results do not depend on the grouping).
     """
     total, world, rank = int(total), int(world), int(rank)
     if world < 1 or not 0 <= rank < world:

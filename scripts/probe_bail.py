@@ -44,3 +44,4 @@ print(f'  flipping-edge |residual| max: <1e-12 {s[16]}, <1e-9 {s[17]}, <1e-6 {s[
       flush=True)
 print(f'  first stage of the step {s[21]} (with >= 2 contacts {s[22]}), stage 4 {s[23]}', flush=True)
 print(f'  by stage e = 1, 2, 3: {s[24]} {s[25]} {s[26]}; e = 5, 6, 7: {s[27]} {s[28]} {s[29]}; e >= 8: {s[30]}', flush=True)
+print(f'  (local loop) flipped edges per iterating lane: one {s[1]}, two {s[2]}, more {s[3]}', flush=True)
