@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define OGBX_ABI_VERSION 3
+#define OGBX_ABI_VERSION 4
 
 typedef enum {
   OGBX_OK = 0,
@@ -297,6 +297,17 @@ typedef struct {
                                 valid_traj_end) interleaved: the drawn index and
                                 its trajectory end in ONE 16-B load (one line per
                                 pick instead of two); used when non-NULL         */
+  /* Optional closed form of the tables (0 = use them).  When the buffer is
+   * num_rows / period equal trajectories whose pickable rows (valid_idxs, or
+   * every row) are the first period_picks rows of each period and whose
+   * trajectory end is row period_end of it, pick p of period q = p /
+   * period_picks maps to idx = q period + p % period_picks and traj_end =
+   * q period + period_end: no index load.  The caller guarantees equality
+   * with valid_idxs / traj_end (ogbench_amd.datasets checks on the device);
+   * the tables stay required for explicit idxs. */
+  int64_t period;
+  int64_t period_picks;
+  int64_t period_end;
 } ogbx_gc_buffer;
 
 /* Goal-sampling configuration (GCDataset config keys, datasets.py:155-170).

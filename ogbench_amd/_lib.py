@@ -173,8 +173,19 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        # struct layouts follow the header's ABI version: a library built
+        # from another version would misread them
+        want = header_abi_version()
+        if handle.ogbx_abi_version() != want:
+            raise RuntimeError(f'{LIB_PATH} has ABI version {handle.ogbx_abi_version()}, {HEADER_PATH} '
+                               f'declares {want}; rebuild it (make -C ogbench_amd/csrc)')
         _lib = handle
         return _lib
+
+
+def header_abi_version(header_path=HEADER_PATH):
+    """OGBX_ABI_VERSION as include/ogbx.h defines it."""
+    return int(re.search(r'#define\s+OGBX_ABI_VERSION\s+(\d+)', open(header_path).read()).group(1))
 
 
 def declared_symbols(header_path=HEADER_PATH):

@@ -65,10 +65,32 @@ __device__ inline int64_t sample_goal(int64_t idx, int64_t final_idx, const Goal
 // random goals valid_idxs[goal pick] (datasets.py:65-70, 307-309).  Every
 // condition is wave-uniform (pointer presence), so no load address waits on
 // another load; for explicit idxs (pick < 0) the end needs idx first.
+// Periodic buffer (ogbx_gc_buffer.period > 0): pick p lies in period
+// q = p / period_picks at offset r, so idx = q period + r and its trajectory
+// end is q period + period_end -- no index load at all.  The IEEE quotient is
+// off by at most one near an integer; the remainder test corrects it.
+__device__ inline int64_t periodic_row(const ogbx_gc_buffer& buf, int64_t pick, int64_t* q_out) {
+  int64_t q = (int64_t)((double)pick / (double)buf.period_picks);
+  int64_t r = pick - q * buf.period_picks;
+  if (r < 0) {
+    --q;
+    r += buf.period_picks;
+  } else if (r >= buf.period_picks) {
+    ++q;
+    r -= buf.period_picks;
+  }
+  *q_out = q;
+  return q * buf.period + r;
+}
+
 __device__ inline void index_loads(const ogbx_gc_buffer& buf, bool explicit_idxs, int64_t pick,
                                    int64_t* idx, int64_t* fin) {
   const int64_t* __restrict__ vi = buf.valid_idxs;
-  if (explicit_idxs) {
+  if (!explicit_idxs && buf.period > 0) {
+    int64_t q;
+    *idx = periodic_row(buf, pick, &q);
+    *fin = q * buf.period + buf.period_end;
+  } else if (explicit_idxs) {
     *fin = buf.traj_end[*idx];
   } else if (buf.valid_pairs) {
     const longlong2 p = reinterpret_cast<const longlong2*>(buf.valid_pairs)[pick];
@@ -87,6 +109,10 @@ __device__ inline void index_loads(const ogbx_gc_buffer& buf, bool explicit_idxs
 }
 
 __device__ inline int64_t rand_goal_of(const ogbx_gc_buffer& buf, int64_t pick) {
+  if (buf.period > 0) {
+    int64_t q;
+    return periodic_row(buf, pick, &q);
+  }
   if (buf.valid_pairs) return buf.valid_pairs[2 * pick];
   return buf.valid_idxs ? buf.valid_idxs[pick] : pick;
 }
@@ -207,6 +233,20 @@ __device__ inline void tile_philox(uint4 (*wb)[kGcMaxTile], int calls, int n_her
     wb[q][b] = make_uint4(w.x, w.y, w.z, w.w);
   }
 }
+// Tile of this workgroup: consecutive workgroup ids go round-robin to the 8
+// XCDs, each with its own L2, so tiles are numbered XCD-major -- the
+// workgroups of one XCD own a contiguous run of samples and the partial
+// 128-B lines where one sample's output rows meet the next are merged in
+// that XCD's L2 instead of being written back twice.
+__device__ inline int64_t xcd_tile() {
+#ifdef OGBX_GC_NO_XCD
+  return blockIdx.x;
+#endif
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  const int64_t per = nb >> 3, rem = nb & 7, x = b & 7;
+  return x * per + (x < rem ? x : rem) + (b >> 3);
+}
+
 __device__ inline u32x4 tile_word(const uint4 (*wb)[kGcMaxTile], int q, int b) {
   const uint4 v = wb[q][b];
   return u32x4{v.x, v.y, v.z, v.w};
@@ -220,7 +260,7 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
     double* masks, double* rewards, ogbx_gc_draw_record rec, bool flat4) {
   __shared__ int64_t sel[4][kGcMaxTile];
   __shared__ uint4 wb[(!kInj && kGcSpread) ? 5 : 1][kGcMaxTile];
-  const int64_t base = (int64_t)blockIdx.x * tile;
+  const int64_t base = xcd_tile() * tile;
   int n_here = (int)((total - base) < tile ? (total - base) : tile);
   if (!kInj && kGcSpread) {
     tile_philox(wb, 5, n_here, base, call_lo, call_hi, k0, k1);
@@ -317,7 +357,7 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     ogbx_hgc_draw_record rec, bool flat4) {
   __shared__ int64_t sel[kHgcSel][kGcMaxTile];
   __shared__ uint4 wb[(!kInj && kGcSpread) ? 7 : 1][kGcMaxTile];
-  const int64_t base = (int64_t)blockIdx.x * tile;
+  const int64_t base = xcd_tile() * tile;
   const int n_here = (int)((total - base) < tile ? (total - base) : tile);
   if (!kInj && kGcSpread) {
     tile_philox(wb, hc.has_low_value_goals ? 7 : 5, n_here, base, call_lo, call_hi, k0, k1);
@@ -490,6 +530,16 @@ static bool any_draw(const ogbx_gc_draws& d) {
          d.a_pick || d.a_geom || d.a_dist || d.a_u_traj || d.a_u_cur;
 }
 
+// period == 0, or a whole number of periods covering the buffer with the
+// picks and the trajectory end inside one period.
+static bool periodic_ok(const ogbx_gc_buffer& b) {
+  if (b.period == 0) return true;
+  const int64_t npick = b.valid_idxs ? b.num_valid : b.num_rows;
+  return b.period > 0 && b.period_picks > 0 && b.period_picks <= b.period && b.period_end >= 0 &&
+         b.period_end < b.period && b.num_rows % b.period == 0 &&
+         npick == (b.num_rows / b.period) * b.period_picks;
+}
+
 extern "C" {
 
 ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
@@ -505,6 +555,7 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
   OGBX_CHECK(buf->num_rows > 0 && buf->traj_end, OGBX_EINVAL, "empty trajectory buffer");
   OGBX_CHECK(buf->valid_idxs == nullptr || buf->num_valid > 0, OGBX_EINVAL,
              "no valid transitions in the dataset");
+  OGBX_CHECK(periodic_ok(*buf), OGBX_EINVAL, "ogbx_gc_buffer: inconsistent period fields");
   GcColumns cc{};
   for (int i = 0; i < num_cols; ++i) {
     OGBX_CHECK(cols[i].src_stride == 0 || cols[i].src_stride >= cols[i].row_bytes, OGBX_EINVAL,
@@ -562,6 +613,7 @@ ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg
   OGBX_CHECK(buf->num_rows > 0 && buf->traj_end, OGBX_EINVAL, "empty trajectory buffer");
   OGBX_CHECK(buf->valid_idxs == nullptr || buf->num_valid > 0, OGBX_EINVAL,
              "no valid transitions in the dataset");
+  OGBX_CHECK(periodic_ok(*buf), OGBX_EINVAL, "ogbx_gc_buffer: inconsistent period fields");
   GcColumns cc{};
   for (int i = 0; i < num_cols; ++i) {
     OGBX_CHECK(cols[i].src_stride == 0 || cols[i].src_stride >= cols[i].row_bytes, OGBX_EINVAL,

@@ -42,6 +42,42 @@ class GcColumn(ctypes.Structure):
     ]
 
 
+def periodic_layout(num_rows, valid, ends):
+    """(period, picks per period, trajectory-end offset) when the buffer is a
+    run of equal trajectories -- the OGBench layout: every episode the same
+    length, its last row invalid -- else (0, 0, 0).  ``valid``: valid_idxs or
+    None (every row pickable); ``ends``: the trajectory end of every pick.
+    The kernels then compute a pick's row and trajectory end instead of
+    loading them (``ogbx_gc_buffer.period``).  Accepted only if the closed
+    form equals ``valid`` and ``ends`` for every pick (checked where the
+    tensors live), so the samples are identical either way."""
+    torch = _torch()
+    R = int(num_rows)
+    if valid is not None:
+        V = valid.numel()
+        ntraj = R - V  # one invalid row per trajectory
+        if ntraj <= 0 or R % ntraj or V % ntraj:
+            return (0, 0, 0)
+        P, pp = R // ntraj, V // ntraj
+    else:
+        if ends.numel() != R:
+            return (0, 0, 0)
+        P = int(ends[0]) + 1
+        if R % P:
+            return (0, 0, 0)
+        pp = P
+    E = int(ends[0])
+    if not 0 <= E < P:
+        return (0, 0, 0)
+    k = torch.arange(ends.numel(), dtype=torch.int64, device=ends.device)
+    q = torch.div(k, pp, rounding_mode='floor')
+    if valid is not None and not torch.equal(q * P + (k - q * pp), valid):
+        return (0, 0, 0)
+    if not torch.equal(q * P + E, ends):
+        return (0, 0, 0)
+    return (P, pp, E)
+
+
 class GcBuffer(ctypes.Structure):
     _fields_ = [
         ('num_rows', ctypes.c_int64),
@@ -50,6 +86,9 @@ class GcBuffer(ctypes.Structure):
         ('traj_end', ctypes.c_void_p),
         ('valid_traj_end', ctypes.c_void_p),
         ('valid_pairs', ctypes.c_void_p),
+        ('period', ctypes.c_int64),
+        ('period_picks', ctypes.c_int64),
+        ('period_end', ctypes.c_int64),
     ]
 
 
@@ -237,10 +276,11 @@ class GCDataset:
         self.valid_traj_end = self.traj_end[valid].contiguous() if valid is not None else None
         # (index, trajectory end) of every valid row interleaved: one 16-B load per pick
         self.valid_pairs = torch.stack([valid, self.valid_traj_end], 1).contiguous() if valid is not None else None
+        self.period = periodic_layout(self.size, valid, self.valid_traj_end if valid is not None else self.traj_end)
         self._buf = GcBuffer(self.size, valid.data_ptr() if valid is not None else None,
                              valid.numel() if valid is not None else 0, self.traj_end.data_ptr(),
                              self.valid_traj_end.data_ptr() if valid is not None else None,
-                             self.valid_pairs.data_ptr() if valid is not None else None)
+                             self.valid_pairs.data_ptr() if valid is not None else None, *self.period)
         self._valid = valid
         self._record, self._rec_off = self._row_record(dataset)
 

@@ -10,7 +10,7 @@ from ogbench_amd import _lib
 
 def test_library_loads_and_reports_abi():
     L = _lib.lib()
-    assert L.ogbx_abi_version() == 3
+    assert L.ogbx_abi_version() == 4
     assert L.ogbx_build_arch() == b'gfx950'
 
 

@@ -173,3 +173,34 @@ def test_out_reuse_matches_fresh_calls(gpu, gold):
     assert b2 is a2 and all(v.data_ptr() == ptrs[k] for k, v in b2.items())
     for k in b1:
         assert torch.equal(b1[k], b2[k]), k
+
+
+def test_periodic_closed_form_matches_tables(gpu):
+    """The OGBench layout (equal trajectories, last row invalid) is sampled
+    through the closed form (ogbx_gc_buffer.period, no index loads); the same
+    dataset with the closed form switched off (tables) gives identical
+    batches, for GC and HGC."""
+    from ogbench_amd.datasets import HGCDataset
+
+    n_traj, L = 40, 250
+    R = n_traj * L
+    g = torch.Generator(device=gpu).manual_seed(5)
+    term = torch.zeros(R, device=gpu)
+    term[L - 1 :: L] = 1
+    data = dict(observations=torch.randn(R, 69, device=gpu, generator=g),
+                actions=torch.randn(R, 21, device=gpu, generator=g),
+                terminals=torch.clamp(term + torch.cat([term[1:], torch.ones(1, device=gpu)]), max=1.0),
+                valids=1.0 - term)
+    from test_oracle_hgc import HGC_CONFIGS
+
+    cases = [(GCDataset, dict(c, p_aug=None, frame_stack=None)) for c in CONFIGS.values()]
+    cases += [(HGCDataset, dict(c, p_aug=None)) for c in HGC_CONFIGS.values()]
+    for cls, cfg in cases:
+        a = cls(Dataset(data, device=gpu), cfg, seed=4)
+        b = cls(Dataset(data, device=gpu), cfg, seed=4)
+        assert a.period == (L, L - 1, L - 2)
+        b._buf.period = b._buf.period_picks = b._buf.period_end = 0
+        for B, nb in ((1024, 1), (96, 3), (4096, 16)):
+            x, y = a.sample(B, num_batches=nb), b.sample(B, num_batches=nb)
+            for k in x:
+                assert torch.equal(x[k], y[k]), (cls.__name__, B, k)

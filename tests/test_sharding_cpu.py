@@ -108,3 +108,4 @@ def test_gloo_world2_sharded_eval_equals_single_run():
         assert np.array_equal(got, ref['obs'][:, b:b + n])
         assert np.array_equal(np.array(total), ref_cnt)
         assert np.array_equal(np.array(per_rank).sum(0), ref_cnt)
+
