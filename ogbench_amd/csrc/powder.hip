@@ -1142,6 +1142,14 @@ extern "C" ogbx_status ogbx_diag_pwf_stamps(unsigned long long* out) {
 }
 #endif
 
+#ifdef OGBX_PWF_RULE_STAMPS
+extern "C" ogbx_status ogbx_diag_pwf_rules(unsigned long long* out) {
+  OGBX_HIP(hipDeviceSynchronize());
+  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(ogbx::g_pwf_rule), 4096 * 16 * sizeof(unsigned long long)));
+  return OGBX_OK;
+}
+#endif
+
 ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int32_t device,
                                ogbx_powder_t* out) {
   OGBX_CHECK(opts && out, OGBX_EINVAL, "ogbx_powder_create: null argument");

@@ -104,6 +104,27 @@ __device__ __forceinline__ float fdens(uint32_t a) { return (float)((kDensPacked
 __device__ __forceinline__ uint32_t dens_i(uint32_t a) { return (uint32_t)(kDensPacked >> (3u * (a & 31u))) & 7u; }
 
 constexpr uint32_t bit(int id) { return 1u << id; }
+
+#ifdef OGBX_PWF_RULE_STAMPS
+// Diagnostic build only: shader-clock cycles per rule, accumulated per env
+// (workgroup) over every forward: slots 0 presence + rands, 1 stone, 2 gravity,
+// 3 sand, 4 fluid, 5 ice, 6 water, 7 fire, 8 plant, 9 velocity, 15 forwards.
+__device__ unsigned long long g_pwf_rule[4096 * 16];
+#define OGBX_RS_BEGIN() unsigned long long _rs_prev = __builtin_amdgcn_s_memtime()
+#define OGBX_RS(slot)                                                                         \
+  do {                                                                                        \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                               \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_pwf_rule[blockIdx.x * 16 + (slot)] += _t - _rs_prev; \
+    _rs_prev = _t;                                                                            \
+  } while (0)
+#else
+#define OGBX_RS_BEGIN() \
+  do {                  \
+  } while (0)
+#define OGBX_RS(slot) \
+  do {                \
+  } while (0)
+#endif
 constexpr uint32_t kVelBit = 1u << 31;  // presence mask: some velocity is nonzero
 
 // Workgroup-level full forward on the LDS state of one world, NT threads.
@@ -820,10 +841,17 @@ struct FullWorld {
 
   __device__ __forceinline__ void forward_rand(const float* __restrict__ src, uint32_t k0, uint32_t k1, uint64_t env, uint32_t ep,
                                uint32_t slot) const {
+    OGBX_RS_BEGIN();
     const uint32_t P = presence();
     if (P & kRandUsers) fill_rands(src, k0, k1, env, ep, slot);  // own cells; presence() synced already
     sync();
+    OGBX_RS(0);
+#ifdef OGBX_PWF_RULE_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_pwf_rule[blockIdx.x * 16 + 15] += 1;
+    forward_masked(P, _rs_prev);
+#else
     forward_masked(P);
+#endif
   }
 
   // HBM <-> LDS for one env's state (bytes, momentum, velocity)
@@ -967,7 +995,11 @@ struct FullWorld {
   static constexpr uint32_t kRandUsers = bit(kSand) | bit(kDust) | kFluidTrig | bit(kIce) | bit(kFire) |
                                          bit(kLava) | bit(kPlant) | bit(kWater);
 
+#ifdef OGBX_PWF_RULE_STAMPS
+  __device__ __forceinline__ void forward_masked(uint32_t P, unsigned long long _rs_prev) const {
+#else
   __device__ __forceinline__ void forward_masked(uint32_t P) const {
+#endif
 #ifdef OGBX_PWF_RULES  // ablation builds (scripts/build_pwf_variants.sh): run only the rules in the mask
     constexpr uint32_t R = OGBX_PWF_RULES;
 #else
@@ -975,8 +1007,11 @@ struct FullWorld {
 #endif
     // R bits: 1 stone, 4 sand, 8 fluid, 16 ice, 32 water, 64 fire, 128 plant, 256 velocity
     if ((R & 1) && (P & bit(kStone))) stone();
+    OGBX_RS(1);
     gravity();
+    OGBX_RS(2);
     if ((R & 4) && (P & (bit(kSand) | bit(kDust)))) sand();
+    OGBX_RS(3);
     if ((R & 8) && (P & kFluidTrig)) {
       fluid();
     } else {
@@ -988,17 +1023,23 @@ struct FullWorld {
       }
       sync();
     }
+    OGBX_RS(4);
     if (P & bit(kIce)) {
       if (R & 16) ice();
       P |= bit(kWater);
     }
+    OGBX_RS(5);
     if ((R & 32) && (P & bit(kWater)) && (P & bit(kIce))) water();
+    OGBX_RS(6);
     if (P & (bit(kFire) | bit(kLava))) {
       if (R & 64) fire();
       P |= bit(kFire) | bit(kWater) | bit(kEmpty) | kVelBit;
     }
+    OGBX_RS(7);
     if ((R & 128) && (P & bit(kPlant))) plant();
+    OGBX_RS(8);
     if ((R & 256) && (P & kVelBit)) velocity();
+    OGBX_RS(9);
   }
 
 
