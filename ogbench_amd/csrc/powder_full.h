@@ -19,6 +19,8 @@
 
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace ogbx {
 
 enum PwElem : int {
@@ -27,11 +29,10 @@ enum PwElem : int {
   kLemming = 18
 };
 
-// LDS of one env: 116 KB at 64x64 (one 1024-thread workgroup per CU), 29 KB
-// at 32x32.  Every rule writes its result to the staging copy (a2, m2, v2 or
-// the scratch flags) and the owners copy it back after a barrier, so no
-// per-thread arrays are needed: loops over a thread's cells stay rolled and
-// the register footprint small.
+// LDS of one env: the state (id|flags, momentum, velocity), the goal ids, the
+// rand decision bits and the rule scratch.  A rule's moves are decided by each
+// cell's owner from the old state and held in registers across one barrier
+// (Moves / commit_moved); conversions go through the scratch flags.
 template <int WS>
 struct alignas(16) PwFullShared {
   static constexpr int C = WS * WS;
@@ -40,14 +41,10 @@ struct alignas(16) PwFullShared {
   alignas(16) float2 v[C];
   alignas(16) uint8_t g[C];    // this env's goal ids
   alignas(16) uint16_t rb[C];  // rand decision bits of the current forward (rand_bits)
-  alignas(16) uint8_t a2[C];   // staging copy of the state (moves)
-  alignas(16) int8_t m2[C];
-  alignas(16) float2 v2[C];
   union {
     struct {  // rule scratch
       alignas(16) uint8_t f1[C];
       alignas(16) uint8_t f2[C];
-      alignas(16) int16_t cnt[C];
       alignas(16) int8_t sw[C];
     };
     alignas(16) uint32_t ob[C * 6 / 4];  // observation staging (between forwards)
@@ -136,6 +133,9 @@ struct FullWorld {
   static constexpr int H = WS, W = WS, C = WS * WS, CPT = C / NT, RPK = NT / W;
   static_assert(NT % W == 0 && CPT * RPK == H, "whole rows per slab");
   static_assert(64 % W == 0, "a wave holds whole rows (fluid row skipping)");
+  static_assert(CPT <= 8, "per-cell codes are packed 8 bits per cell in Codes");
+  // 8 bits per cell of the thread (conversion codes, angle bins)
+  using Codes = typename std::conditional<(CPT <= 4), uint32_t, uint64_t>::type;
   PwFullShared<WS>& s;
   mutable int r0, col;
   __device__ __forceinline__ explicit FullWorld(PwFullShared<WS>& sh)
@@ -234,38 +234,33 @@ struct FullWorld {
   }
 
   // ------------------------------------------------------------- rules
-  // Staged writes: stage(i, ...) into the copy, commit() copies own cells back.
-  __device__ __forceinline__ void stage(int i, uint32_t a, int m, float2 v) const {
-    s.a2[i] = (uint8_t)a;
-    s.m2[i] = (int8_t)m;
-    s.v2[i] = v;
+  // Moves: the owner of each cell decides its new value from the old state
+  // and holds it in registers across the barrier that separates the rule's
+  // reads from its writes (no LDS staging copy of the world).
+  struct Moves {
+    uint32_t am[CPT];  // id|flags byte | momentum byte << 8
+    float2 v[CPT];
+    uint32_t moved = 0;
+  };
+  __device__ static __forceinline__ void take(Moves& mv, int k, uint32_t a, int m, float2 v) {
+    mv.am[k] = (a & 0xFFu) | (((uint32_t)m & 0xFFu) << 8);
+    mv.v[k] = v;
+    mv.moved |= 1u << k;
   }
-  __device__ __forceinline__ void stage_from(int i, int j) const { stage(i, s.a[j], s.m[j], s.v[j]); }
-  __device__ __forceinline__ void commit() const {
-    fence_idx();
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      s.a[i] = s.a2[i];
-      s.m[i] = s.m2[i];
-      s.v[i] = s.v2[i];
-    }
-    sync();
-  }
-  // Copy back only the cells that moved (bit k of `moved`); the others get
-  // own(i), an in-place update of the cell itself (or nothing).
+  __device__ __forceinline__ void take_from(Moves& mv, int k, int j) const { take(mv, k, s.a[j], s.m[j], s.v[j]); }
+  // Write the moved cells (bit k of mv.moved); the others get own(i), an
+  // in-place update of the cell itself (or nothing).
   template <typename Own>
-  __device__ __forceinline__ void commit_moved(uint32_t moved, Own own) const {
+  __device__ __forceinline__ void commit_moved(const Moves& mv, Own own) const {
     fence_idx();
     sync();
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
-      if ((moved >> k) & 1u) {
-        s.a[i] = s.a2[i];
-        s.m[i] = s.m2[i];
-        s.v[i] = s.v2[i];
+      if ((mv.moved >> k) & 1u) {
+        s.a[i] = (uint8_t)mv.am[k];
+        s.m[i] = (int8_t)(mv.am[k] >> 8);
+        s.v[i] = mv.v[k];
       } else {
         own(i);
       }
@@ -287,6 +282,7 @@ struct FullWorld {
 
   __device__ __forceinline__ void stone() const {
     fence_idx();
+    uint32_t na[CPT];
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
@@ -297,11 +293,11 @@ struct FullWorld {
         const int sup = ((jl >= 0) & (fid(al) == kStone)) + ((jr >= 0) & (fid(ar) == kStone));
         a = (a & ~kGrav) | (sup < 2 ? kGrav : 0u);
       }
-      s.a2[i] = (uint8_t)a;
+      na[k] = a;
     }
     sync();
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) s.a[cell(k)] = s.a2[cell(k)];
+    for (int k = 0; k < CPT; ++k) s.a[cell(k)] = (uint8_t)na[k];
     sync();
   }
 
@@ -318,7 +314,7 @@ struct FullWorld {
     asm volatile("; GRAV_BEGIN");
 #endif
     fence_idx();
-    uint32_t moved = 0;
+    Moves mv;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k), up = nb(k, -1, 0), up2 = nb(k, -2, 0), dn = nb(k, 1, 0);
@@ -326,11 +322,10 @@ struct FullWorld {
       const bool down = d0 & !d1, raised = d1 & !d2;
       if (down | raised) {
         const int j = down ? dn : up;
-        stage(i, rd(s.a[j]) | (raised ? kDidg : 0u), s.m[j], s.v[j]);
-        moved |= 1u << k;
+        take(mv, k, rd(s.a[j]) | (raised ? kDidg : 0u), s.m[j], s.v[j]);
       }
     }
-    commit_moved(moved, [&](int i) { s.a[i] = (uint8_t)rd(s.a[i]); });
+    commit_moved(mv, [&](int i) { s.a[i] = (uint8_t)rd(s.a[i]); });
   }
 
   __device__ __forceinline__ void sand() const {
@@ -342,7 +337,7 @@ struct FullWorld {
     for (int pass = 0; pass < 2; ++pass) {
       const int go = pass == 0 ? -1 : 1;        // fall toward -1 (left) then +1 (right)
       const uint32_t fl = pass == 0 ? 1u : 0u;  // fall_dir: rm > 0.5, then rm <= 0.5
-      uint32_t moved = 0;
+      Moves mvs;
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), ibl = nb(k, 1, go), iar = nb(k, -1, -go);
@@ -353,12 +348,9 @@ struct FullWorld {
         const bool f_own = (s.rb[i] & 1u) == fl, f_ar = (s.rb[iar] & 1u) == fl;
         const bool mv = elem & !fdidg(bl) & f_own & (dens_i(a) > dens_i(bl)) & (bool)fgrav(bl) & ndg;
         const bool in = elem_ar & !fdidg(ar) & f_ar & (dens_i(ar) > dens_i(a)) & (bool)fgrav(ar) & ndg;
-        if (mv | in) {
-          stage_from(i, mv ? ibl : iar);
-          moved |= 1u << k;
-        }
+        if (mv | in) take_from(mvs, k, mv ? ibl : iar);
       }
-      commit_moved(moved, [](int) {});
+      commit_moved(mvs, [](int) {});
     }
   }
 
@@ -386,8 +378,27 @@ struct FullWorld {
     const int lane = (int)(threadIdx.x & 63u);
     return (lane & (63 & ~(W - 1))) | ((lane + dc) & (W - 1));
   }
+  // One lane rotation of the wave (gfx9 DPP wave_rol / wave_ror): the value of
+  // lane (lane + 1) mod 64 / (lane - 1) mod 64.  At W = 64 a wave is exactly
+  // one row, so this is the periodic row neighbour with no LDS round trip.
+  __device__ static __forceinline__ int wave_rot(int x, bool next) {
+    return next ? __builtin_amdgcn_update_dpp(0, x, 0x134, 0xF, 0xF, false)
+                : __builtin_amdgcn_update_dpp(0, x, 0x13C, 0xF, 0xF, false);
+  }
   template <typename T>
-  __device__ __forceinline__ T rowx(T x, int dc) const { return __shfl(x, row_lane(dc), 64); }
+  __device__ __forceinline__ T rowx(T x, int dc) const {
+    static_assert(sizeof(T) == 4, "32-bit lanes");
+    if constexpr (W == 64) {
+      // dc in {-2, -1, 1, 2}, a constant after unrolling; every lane active
+      int y = __builtin_bit_cast(int, x);
+      const bool next = dc > 0;
+      y = wave_rot(y, next);
+      if (dc == 2 || dc == -2) y = wave_rot(y, next);
+      return __builtin_bit_cast(T, y);
+    } else {
+      return __shfl(x, row_lane(dc), 64);
+    }
+  }
 
   // FluidFlow (sim.py:593-667) in registers: fluid moves never leave a row and
   // a wave holds whole rows, so each wave runs both passes on its rows with
@@ -489,7 +500,7 @@ struct FullWorld {
 #ifdef OGBX_ASM_MARKS
     asm volatile("; FIRE_BEGIN");
 #endif
-    static_assert(CPT <= 4, "conversion codes packed 8 bits per cell");
+    static_assert(CPT <= 8, "conversion codes packed 8 bits per cell");
     fence_idx();
     uint64_t* hotm = s.rowm[0];   // fire | lava before the burn
     uint64_t* burnm = s.rowm[1];  // burnable cells after the burn
@@ -504,7 +515,7 @@ struct FullWorld {
     sync();
     // burn decisions; f2 bit 0: burns (pushes its 4 neighbours with 8), bit 1:
     // dust near fire (pushes with 30)
-    uint32_t conv = 0;  // 8 bits per cell: new id + 1, 0 = unchanged
+    Codes conv = 0;  // 8 bits per cell: new id + 1, 0 = unchanged
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
@@ -516,7 +527,7 @@ struct FullWorld {
                         ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p02);
       const bool burn = cand & nr, burn_ice = (id == kIce) & p02 & nr;
       s.f2[i] = (uint8_t)((burn ? 1 : 0) | (((id == kDust) & nr) ? 2 : 0));
-      conv |= (burn ? kFire + 1u : (burn_ice ? kWater + 1u : 0u)) << (8 * k);
+      conv |= (Codes)(burn ? kFire + 1u : (burn_ice ? kWater + 1u : 0u)) << (8 * k);
     }
     sync();
     // impulses away from a burning neighbour (sim.py:744-752): left, above,
@@ -525,7 +536,7 @@ struct FullWorld {
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t L = s.f2[nb(k, 0, -1)], U = s.f2[nb(k, -1, 0)], D = s.f2[nb(k, 1, 0)], R = s.f2[nb(k, 0, 1)];
-      const uint32_t to = (conv >> (8 * k)) & 0xFFu;
+      const uint32_t to = (uint32_t)(conv >> (8 * k)) & 0xFFu;
       if (to) {
         put(i, elem(to - 1));
       } else if ((L | U | D | R) & 3u) {
@@ -562,18 +573,18 @@ struct FullWorld {
     sync();
     // empty cells next to a source ignite (ri < 0.3); fire with re < 0.4 and
     // no burnable neighbour fades to empty (sim.py:778-790)
-    uint32_t conv2 = 0;
+    Codes conv2 = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
       const bool burn_empty = (id == kEmpty) & ri_lt(k, kRi03) & any3x3(srcm, k);
       bool fd = (fade >> k) & 1u;
       if (burn_empty & re_lt(k, kRe04)) fd = !((nbr >> k) & 1u);
-      conv2 |= (fd ? kEmpty + 1u : (burn_empty ? kFire + 1u : 0u)) << (8 * k);
+      conv2 |= (Codes)(fd ? kEmpty + 1u : (burn_empty ? kFire + 1u : 0u)) << (8 * k);
     }
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
-      const uint32_t to = (conv2 >> (8 * k)) & 0xFFu;
+      const uint32_t to = (uint32_t)(conv2 >> (8 * k)) & 0xFFu;
       if (to) put(cell(k), elem(to - 1));
     }
     sync();
@@ -630,7 +641,7 @@ struct FullWorld {
       // f2 = angle bin of cells that may move (mag above the pass threshold, not
       // wall), 0xFF otherwise; sw = chosen swap direction (-1 none)
       uint32_t dirs = 0;  // angle bins present among the cells that may move
-      uint32_t binr = 0;  // 8 bits per cell: bin, 0xFF = cannot move
+      Codes binr = 0;  // 8 bits per cell: bin, 0xFF = cannot move
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
@@ -650,7 +661,7 @@ struct FullWorld {
           b8 = (uint8_t)b;
           dirs |= 1u << b8;
         }
-        binr |= (uint32_t)b8 << (8 * k);
+        binr |= (Codes)b8 << (8 * k);
         s.sw[i] = -1;
         s.f1[i] = 0;
       }
@@ -683,7 +694,7 @@ struct FullWorld {
         uint32_t mk = 0;
 #pragma unroll
         for (int k = 0; k < CPT; ++k) {
-          if (((binr >> (8 * k)) & 0xFFu) == (uint32_t)d) {
+          if (((uint32_t)(binr >> (8 * k)) & 0xFFu) == (uint32_t)d) {
             const int i = cell(k), j = nb(k, dr, dc);
             if ((s.sw[i] == -1) & (s.sw[j] == -1) & (fid(s.a[j]) == kEmpty)) {
               s.f1[i] = (uint8_t)(d + 1);
@@ -702,7 +713,7 @@ struct FullWorld {
         }
         sync();
       }
-      uint32_t moved = 0;
+      Moves mvs;
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
@@ -712,12 +723,11 @@ struct FullWorld {
           dir_of(w, dr, dc);
           const int j = nb(k, dr, dc);
           const float2 old = s.v[i], nv = s.v[j];
-          stage(i, s.a[j], s.m[j], make_float2(nv.x * 0.5f + old.x * 0.5f, nv.y * 0.5f + old.y * 0.5f));
-          moved |= 1u << k;
+          take(mvs, k, s.a[j], s.m[j], make_float2(nv.x * 0.5f + old.x * 0.5f, nv.y * 0.5f + old.y * 0.5f));
         }
       }
       // unswapped cells: v = v * 0.5 + v * 0.5 in place
-      commit_moved(moved, [&](int i) {
+      commit_moved(mvs, [&](int i) {
         float2 v = s.v[i];
         v.x = v.x * 0.5f + v.x * 0.5f;
         v.y = v.y * 0.5f + v.y * 0.5f;
@@ -898,10 +908,8 @@ struct FullWorld {
       const uint32_t gk = s.g[cell(k)];
       const bool m = gk == fid(s.a[cell(k)]) || gk == fid(s.a[nb(k, 0, -1)]) || gk == fid(s.a[nb(k, 0, 1)]) ||
                      gk == fid(s.a[nb(k, -1, 0)]) || gk == fid(s.a[nb(k, 1, 0)]);
-      err += m ? 0 : 1;
+      err += __popcll(__ballot(!m));  // wave-uniform count, no lane shuffles
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) err += __shfl_xor(err, off);
     if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = err;
     sync();
     int total = 0;
@@ -951,6 +959,19 @@ struct FullWorld {
     sync();  // staging shares LDS with the rule scratch
   }
 
+  // OR over the wave with DPP (every lane active): quad butterflies, then the
+  // 8- and 16-lane mirrors leave each 16-lane row's OR in all of its lanes;
+  // the four rows are combined from lanes 0, 16, 32, 48.  No LDS round trip
+  // (__shfl_xor is a ds_bpermute per step).
+  __device__ static __forceinline__ uint32_t wave_or(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    return (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) | __builtin_amdgcn_readlane((int)x, 16) |
+                      __builtin_amdgcn_readlane((int)x, 32) | __builtin_amdgcn_readlane((int)x, 48));
+  }
+
   // Bitmask of the ids present in the world (+ kVelBit if some velocity is
   // nonzero).  A rule whose trigger elements are absent is an identity and is
   // skipped; the mask is then widened by what each executed rule can create.
@@ -963,8 +984,7 @@ struct FullWorld {
       const float2 v = s.v[i];
       m |= bit((int)fid(s.a[i])) | ((v.x != 0.0f || v.y != 0.0f) ? kVelBit : 0u);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off);
+    m = wave_or(m);
     sync();  // red is free
     if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = (int32_t)m;
     sync();
@@ -976,8 +996,7 @@ struct FullWorld {
 
   // OR of a per-thread mask over the workgroup
   __device__ __forceinline__ uint32_t block_or(uint32_t m) const {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m |= __shfl_xor(m, off);
+    m = wave_or(m);
     if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = (int32_t)m;
     sync();
     uint32_t all = 0;
