@@ -224,13 +224,19 @@ constexpr bool kGcSpread = true;
 #else
 constexpr bool kGcSpread = false;
 #endif
+// Every lane of a wave that has a call computes one (lanes past the last call
+// repeat one and store nothing): gfx950 issues a dependent integer chain about
+// twice as slowly with <= 16 active lanes, and a B = 1,024 tile
+// has 5-7 calls.
 __device__ inline void tile_philox(uint4 (*wb)[kGcMaxTile], int calls, int n_here, int64_t base,
                                    uint32_t call_lo, uint32_t call_hi, uint32_t k0, uint32_t k1) {
-  for (int t = threadIdx.x; t < calls * n_here; t += blockDim.x) {
-    const int b = t / calls, q = t - b * calls;
+  const int tot = calls * n_here, span = (tot + 63) & ~63;
+  for (int t = threadIdx.x; t < span; t += blockDim.x) {
+    const int tt = t < tot ? t : t % tot;
+    const int b = tt / calls, q = tt - b * calls;
     const uint64_t su = (uint64_t)(base + b);
     const u32x4 w = philox4x32_10({(uint32_t)su, call_lo, (uint32_t)q, (uint32_t)(su >> 32) ^ call_hi}, k0, k1);
-    wb[q][b] = make_uint4(w.x, w.y, w.z, w.w);
+    if (t < tot) wb[q][b] = make_uint4(w.x, w.y, w.z, w.w);
   }
 }
 // Tile of this workgroup: consecutive workgroup ids go round-robin to the 8
@@ -266,13 +272,17 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
     tile_philox(wb, 5, n_here, base, call_lo, call_hi, k0, k1);
     __syncthreads();
   }
-  if (threadIdx.x < n_here) {
-    const int64_t s = base + threadIdx.x;
+  // The whole first wave runs the sample chains (lane b % n_here; only lanes
+  // b < n_here store): a chain on a few active lanes issues about twice as
+  // slowly on gfx950, and a B = 1,024 tile has one sample.
+  if (threadIdx.x < 64 && n_here > 0) {
+    const int b = (int)threadIdx.x % n_here;
+    const bool own = (int)threadIdx.x < n_here;
+    const int64_t s = base + b;
     const uint64_t su = (uint64_t)s;
     const uint32_t c0 = (uint32_t)su, c3 = (uint32_t)(su >> 32) ^ call_hi;
     u32x4 w0, w1, w2, w3, w4;
     if (!kInj && kGcSpread) {
-      const int b = (int)threadIdx.x;
       w0 = tile_word(wb, 0, b), w1 = tile_word(wb, 1, b), w2 = tile_word(wb, 2, b), w3 = tile_word(wb, 3, b),
       w4 = tile_word(wb, 4, b);
     } else {
@@ -307,10 +317,11 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
                                    cfg.value_traj_thresh, cfg.value_geom_sample, cfg.value_cur_is_one);
     const int64_t ag = sample_goal(idx, final_idx, a, a_rand, cfg.actor_p_curgoal,
                                    cfg.actor_traj_thresh, cfg.actor_geom_sample, cfg.actor_cur_is_one);
-    sel[0][threadIdx.x] = idx;
-    sel[1][threadIdx.x] = next;
-    sel[2][threadIdx.x] = vg;
-    sel[3][threadIdx.x] = ag;
+    if (own) {
+    sel[0][b] = idx;
+    sel[1][b] = next;
+    sel[2][b] = vg;
+    sel[3][b] = ag;
     if (idxs_out) idxs_out[s] = idx;
     if (vgoal_out) vgoal_out[s] = vg;
     if (agoal_out) agoal_out[s] = ag;
@@ -330,6 +341,7 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
       rec.a_u_traj[s] = a.u_traj;
       rec.a_u_cur[s] = a.u_cur;
     }
+    }  // own
   }
   __syncthreads();
   copy_tile<0>(cols, num_cols, sel, base, n_here, flat4);
@@ -363,13 +375,14 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     tile_philox(wb, hc.has_low_value_goals ? 7 : 5, n_here, base, call_lo, call_hi, k0, k1);
     __syncthreads();
   }
-  if (threadIdx.x < n_here) {
-    const int64_t s = base + threadIdx.x;
+  if (threadIdx.x < 64 && n_here > 0) {  // the whole first wave: see gc_sample_kernel
+    const int b = (int)threadIdx.x % n_here;
+    const bool own = (int)threadIdx.x < n_here;
+    const int64_t s = base + b;
     const uint64_t su = (uint64_t)s;
     const uint32_t c0 = (uint32_t)su, c3 = (uint32_t)(su >> 32) ^ call_hi;
     u32x4 w0, w1, w2, w3, w4;
     if (!kInj && kGcSpread) {
-      const int b = (int)threadIdx.x;
       w0 = tile_word(wb, 0, b), w1 = tile_word(wb, 1, b), w2 = tile_word(wb, 2, b), w3 = tile_word(wb, 3, b),
       w4 = tile_word(wb, 4, b);
     } else {
@@ -391,8 +404,8 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     int64_t l_rand = 0;
     if (hc.has_low_value_goals) {
       if (!kInj && kGcSpread) {
-        w5 = tile_word(wb, 5, (int)threadIdx.x);
-        w6 = tile_word(wb, 6, (int)threadIdx.x);
+        w5 = tile_word(wb, 5, b);
+        w6 = tile_word(wb, 6, b);
       } else {
         w5 = philox4x32_10({c0, call_lo, 5u, c3}, k0, k1);
         w6 = philox4x32_10({c0, call_lo, 6u, c3}, k0, k1);
@@ -425,7 +438,7 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
       l.u_cur = (kInj && dr.l_u_cur) ? dr.l_u_cur[s] : u01_from(w6.z, w6.w);
       lvg = sample_goal(idx, fin, l, l_rand, cfg.value_p_curgoal, cfg.value_traj_thresh, 1,
                         cfg.value_cur_is_one);
-      if (rec.l_pick) {
+      if (rec.l_pick && own) {
         rec.l_pick[s] = l.pick;
         rec.l_geom[s] = l.geom;
         rec.l_u_traj[s] = l.u_traj;
@@ -438,7 +451,8 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
     high_next(idx, fin, hag, hc.actor_subgoal_steps, &ha_next, &ha_steps);
     const int64_t la_goal = idx + hc.actor_subgoal_steps < fin ? idx + hc.actor_subgoal_steps : fin;
     high_next(idx, fin, hag, hc.low_subgoal_steps, &la_next, &la_steps);
-    const int t = threadIdx.x;
+    if (own) {
+    const int t = b;
     sel[0][t] = idx;
     sel[1][t] = next;
     sel[2][t] = hvg;
@@ -483,6 +497,7 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
       rec.gc.a_u_traj[s] = a.u_traj;
       rec.gc.a_u_cur[s] = a.u_cur;
     }
+    }  // own
   }
   __syncthreads();
   copy_tile<0>(cols, num_cols, sel, base, n_here, flat4);
