@@ -52,7 +52,9 @@ struct alignas(16) PwFullShared {
   uint32_t lut[32];
   int32_t elem_ids[8];
   float vel_q[8];  // angle-bin thresholds on q (PowderParams::vel_q)
-  int32_t red[16];
+  int32_t red[16];    // presence()
+  int32_t red_e[16];  // errors()
+  int32_t red_v[16];  // block_or()
   uint64_t rowm[3][WS];  // per-row cell bitmasks (bit c = column c) of rule predicates
 };
 
@@ -267,19 +269,6 @@ struct FullWorld {
     }
     sync();
   }
-  // element conversions: f1[i] = new id + 1 (0 = unchanged) -> own cells
-  __device__ __forceinline__ void commit_conversions() const {
-    fence_idx();
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      const uint32_t to = s.f1[i];
-      if (to) put(i, elem(to - 1));
-    }
-    sync();
-  }
-
   __device__ __forceinline__ void stone() const {
     fence_idx();
     uint32_t na[CPT];
@@ -468,9 +457,9 @@ struct FullWorld {
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
       const bool to = (id == kIce) & ri_lt(k, kRi002) & (count3x3(melt, k) > 1);
-      s.f1[cell(k)] = to ? kWater + 1 : 0;
+      if (to) put(cell(k), elem(kWater));  // decided from masks only: in place
     }
-    commit_conversions();
+    sync();
   }
 
   __device__ __forceinline__ void water() const {
@@ -482,9 +471,9 @@ struct FullWorld {
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
       const bool to = (id == kWater) & re_lt(k, kRe005) & (count3x3(ice, k) >= 3);
-      s.f1[cell(k)] = to ? kIce + 1 : 0;
+      if (to) put(cell(k), elem(kIce));  // decided from masks only: in place
     }
-    commit_conversions();
+    sync();
   }
 
   __device__ static __forceinline__ bool burnable(uint32_t x) {
@@ -529,6 +518,12 @@ struct FullWorld {
       s.f2[i] = (uint8_t)((burn ? 1 : 0) | (((id == kDust) & nr) ? 2 : 0));
       conv |= (Codes)(burn ? kFire + 1u : (burn_ice ? kWater + 1u : 0u)) << (8 * k);
     }
+    // burnable cells of the post-burn world (the owner knows its cell's
+    // conversion already), published with the burn flags
+    row_masks(burnm, [&](int k) {
+      const uint32_t to = (uint32_t)(conv >> (8 * k)) & 0xFFu;
+      return burnable(to ? to - 1 : fid(s.a[cell(k)]));
+    });
     sync();
     // impulses away from a burning neighbour (sim.py:744-752): left, above,
     // below, right; then the conversions (own cells, in place)
@@ -552,10 +547,7 @@ struct FullWorld {
         s.v[i] = v;
       }
     }
-    sync();
-    // burnable neighbour counts on the post-burn world
-    row_masks(burnm, [&](int k) { return burnable(fid(s.a[cell(k)])); });
-    sync();
+    // (no barrier: the steps below read only own cells and the row masks)
     // fire spread sources: (fire or lava before the burn) with a burnable
     // neighbour, and lava; fading fire (no burnable neighbour)
     uint32_t fade = 0, nbr = 0;  // bit k: some burnable cell in the 3x3
@@ -612,10 +604,10 @@ struct FullWorld {
       bool to_plant = grow && cnt <= 3 && cnt >= 1;
       const bool to_empty = grow && cnt > 3;
       if (seed && cnt > 0) to_plant = any3x3(iwm, k);
-      const int to = to_plant ? kPlant + 1 : (to_empty ? kEmpty + 1 : 0);
-      s.f1[cell(k)] = (uint8_t)to;
+      // decided from the own cell and the row masks only: converted in place
+      if (to_plant | to_empty) put(cell(k), elem(to_plant ? (uint32_t)kPlant : (uint32_t)kEmpty));
     }
-    commit_conversions();
+    sync();
   }
 
   // direction d (sim.py direction_func) as (dr, dc): 0 right, 1 below-right,
@@ -910,11 +902,11 @@ struct FullWorld {
                      gk == fid(s.a[nb(k, -1, 0)]) || gk == fid(s.a[nb(k, 1, 0)]);
       err += __popcll(__ballot(!m));  // wave-uniform count, no lane shuffles
     }
-    if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = err;
+    if ((threadIdx.x & 63) == 0) s.red_e[threadIdx.x >> 6] = err;
     sync();
     int total = 0;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) total += s.red[w];
+    for (int w = 0; w < NT / 64; ++w) total += s.red_e[w];
     sync();
     return total;
   }
@@ -985,7 +977,7 @@ struct FullWorld {
       m |= bit((int)fid(s.a[i])) | ((v.x != 0.0f || v.y != 0.0f) ? kVelBit : 0u);
     }
     m = wave_or(m);
-    sync();  // red is free
+    // red is free: its last readers (the previous forward) are past many barriers
     if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = (int32_t)m;
     sync();
     uint32_t all = 0;
@@ -994,15 +986,15 @@ struct FullWorld {
     return all;
   }
 
-  // OR of a per-thread mask over the workgroup
+  // OR of a per-thread mask over the workgroup (own slots red_v; a barrier
+  // must separate two calls -- velocity's passes have several between them)
   __device__ __forceinline__ uint32_t block_or(uint32_t m) const {
     m = wave_or(m);
-    if ((threadIdx.x & 63) == 0) s.red[threadIdx.x >> 6] = (int32_t)m;
+    if ((threadIdx.x & 63) == 0) s.red_v[threadIdx.x >> 6] = (int32_t)m;
     sync();
     uint32_t all = 0;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) all |= (uint32_t)s.red[w];
-    sync();  // red is free again
+    for (int w = 0; w < NT / 64; ++w) all |= (uint32_t)s.red_v[w];
     return all;
   }
 
