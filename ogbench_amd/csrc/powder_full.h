@@ -141,12 +141,24 @@ struct FullWorld {
   PwFullShared<WS>& s;
   mutable int r0, col;
   __device__ __forceinline__ explicit FullWorld(PwFullShared<WS>& sh)
-      : s(sh), r0((int)threadIdx.x / W), col((int)threadIdx.x % W) {}
+      : s(sh),
+        r0(W == 64 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / W) : (int)threadIdx.x / W),
+        col((int)threadIdx.x % W) {}
 
   // Opaque redefinition of the thread's coordinates: cell/neighbour indices are
   // recomputed after it instead of being hoisted (as VGPRs) across the whole
-  // forward by loop-invariant code motion.
-  __device__ __forceinline__ void fence_idx() const { asm volatile("" : "+v"(r0), "+v"(col)); }
+  // forward by loop-invariant code motion.  At W = 64 a wave is one row, so the
+  // row is wave-uniform and kept in an SGPR: every row term of a cell or
+  // neighbour index is scalar arithmetic, and only the column is per lane.
+  __device__ __forceinline__ void fence_idx() const {
+    if constexpr (W == 64) {
+      int t = __builtin_amdgcn_readfirstlane(r0);
+      asm volatile("" : "+s"(t), "+v"(col));
+      r0 = t;
+    } else {
+      asm volatile("" : "+v"(r0), "+v"(col));
+    }
+  }
   __device__ __forceinline__ int row(int k) const { return r0 + k * RPK; }
   __device__ __forceinline__ int cell(int k) const { return row(k) * W + col; }
   // periodic neighbour (np.roll semantics)
