@@ -650,9 +650,12 @@ struct FullWorld {
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k);
         const float2 v = s.v[i];
-        const float mag = sqrtf(v.x * v.x + v.y * v.y);
+        const float ss = v.x * v.x + v.y * v.y, thr = pass == 0 ? 1.0f : 2.0f;
         uint8_t b8 = 0xFF;
-        if (mag > (pass == 0 ? 1.0f : 2.0f) && fid(s.a[i]) != kWall) {
+        // sqrt is monotone and exact at the squares 1 and 4, so mag > thr
+        // needs ss > thr * thr: only those cells take the root and the quotient
+        const float mag = ss > thr * thr ? sqrtf(ss) : 0.0f;
+        if (mag > thr && fid(s.a[i]) != kWall) {
           // floor(8 * ang + 0.5) mod 8 with ang from float32 arccos(q): a count
           // of exact float32 thresholds on q (host: vel_bin_thresholds)
           const float q = v.y / (mag + 0.001f);
@@ -826,30 +829,37 @@ struct FullWorld {
   __device__ __forceinline__ bool re_lt(int k, uint32_t cat) const { return ((s.rb[cell(k)] >> 10) & 3u) < cat; }
 
   // Rand decision bits of one forward for this thread's cells: from injected
-  // fields (src = [3, H, W] float32) or Philox (one 4x32 draw per cell).
+  // fields (src = [3, H, W] float32) or Philox (three 4x32 draws per four cells).
+  // Philox: the cells of a column whose rows are congruent mod H/4 form a
+  // group of four (a thread owns whole groups for CPT = 4 or 8, whatever the
+  // thread count), and the group's 12 floats are the 12 words of three calls
+  // with counter (4 g + c, env, episode, slot), g = the group's first cell:
+  // cell j of the group takes words 3j, 3j + 1, 3j + 2 of the calls' 12.
   __device__ __forceinline__ void fill_rands(const float* __restrict__ src, uint32_t k0, uint32_t k1, uint64_t env, uint32_t ep,
                              uint32_t slot) const {
     fence_idx();
+    if (src) {
 #pragma unroll 2
-    for (int k = 0; k < CPT; ++k) {
-      const int i = cell(k);
-      float rm, ri, re;
-      if (src) {
-        rm = src[i];
-        ri = src[C + i];
-        re = src[2 * C + i];
-      } else {
-#ifdef OGBX_PWF_ABL_NORAND  // timing ablation: a cheap hash instead of Philox (changes the stream)
-        const uint32_t hh = ((uint32_t)i * 2654435761u) ^ (ep * 40503u) ^ (uint32_t)env ^ slot;
-        const u32x4 w = {hh, hh * 747796405u, hh * 2891336453u, hh};
-#else
-        const u32x4 w = philox4x32_10({(uint32_t)i, (uint32_t)env, ep, slot}, k0 ^ (uint32_t)(env >> 32), k1);
-#endif
-        rm = u01f_from(w.x);
-        ri = u01f_from(w.y);
-        re = u01f_from(w.z);
+      for (int k = 0; k < CPT; ++k) {
+        const int i = cell(k);
+        s.rb[i] = (uint16_t)rand_bits(src[i], src[C + i], src[2 * C + i]);
       }
-      s.rb[i] = (uint16_t)rand_bits(rm, ri, re);
+      return;
+    }
+    static_assert(CPT % 4 == 0, "whole groups of four cells per thread");
+    constexpr int G = CPT / 4;  // groups per thread; member j of group q is cell q + j G
+#pragma unroll 1
+    for (int q = 0; q < G; ++q) {
+      const uint32_t g = (uint32_t)cell(q);  // row(q) < H / 4: the group's first cell
+      uint32_t w[12];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const u32x4 x = philox4x32_10({4u * g + (uint32_t)c, (uint32_t)env, ep, slot}, k0 ^ (uint32_t)(env >> 32), k1);
+        w[4 * c] = x.x, w[4 * c + 1] = x.y, w[4 * c + 2] = x.z, w[4 * c + 3] = x.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        s.rb[cell(q + j * G)] = (uint16_t)rand_bits(u01f_from(w[3 * j]), u01f_from(w[3 * j + 1]), u01f_from(w[3 * j + 2]));
     }
   }
 
