@@ -579,6 +579,7 @@ __device__ __forceinline__ void pwf_tables(PwFullShared<WS>& sh, const PowderPar
   if (t < 32) sh.lut[t] = Pp->lut[t];
   if (t < 8) sh.elem_ids[t] = Pp->elem_ids[t];
   if (t < 8) sh.vel_q[t] = Pp->vel_q[t];
+  if (t < 3) sh.rowm[t][0] = sh.rowm[t][WS + 1] = 0ull;  // zero padding rows
   __syncthreads();
 }
 

@@ -55,7 +55,10 @@ struct alignas(16) PwFullShared {
   int32_t red[16];    // presence()
   int32_t red_e[16];  // errors()
   int32_t red_v[16];  // block_or()
-  uint64_t rowm[3][WS];  // per-row cell bitmasks (bit c = column c) of rule predicates
+  // per-row cell bitmasks (bit c = column c) of rule predicates, rows -1..H:
+  // rows -1 and H are zero padding (pwf_tables), so 3x3 queries read three
+  // rows with no bounds branch
+  uint64_t rowm[3][WS + 2];
 };
 
 // render colours as float32 c / 255 (sim.py:402-453), velocity colour
@@ -103,6 +106,9 @@ __device__ __forceinline__ float fdens(uint32_t a) { return (float)((kDensPacked
 __device__ __forceinline__ uint32_t dens_i(uint32_t a) { return (uint32_t)(kDensPacked >> (3u * (a & 31u))) & 7u; }
 
 constexpr uint32_t bit(int id) { return 1u << id; }
+// id in a set of ids: one shift of the set's mask (a compare chain costs a
+// v_cmp + v_cndmask per member)
+__device__ __forceinline__ bool in_set(uint32_t mask, uint32_t id) { return (mask >> (id & 31u)) & 1u; }
 
 #ifdef OGBX_PWF_RULE_STAMPS
 // Diagnostic build only: shader-clock cycles per rule, accumulated per env
@@ -219,9 +225,10 @@ struct FullWorld {
       }
     }
   }
-  // bits (c-1, c, c+1) of row r's mask, zero outside the world
+  // row masks of buffer b, indexable by rows -1..H
+  __device__ __forceinline__ uint64_t* rmask(int b) const { return s.rowm[b] + 1; }
+  // bits (c-1, c, c+1) of row r's mask (zero outside the world: padding rows)
   __device__ __forceinline__ uint32_t win3(const uint64_t* rm, int r) const {
-    if ((unsigned)r >= (unsigned)H) return 0u;
     const uint64_t x = rm[r];
     return (uint32_t)((col == 0 ? x << 1 : x >> (col - 1)) & 7u);
   }
@@ -234,9 +241,7 @@ struct FullWorld {
       // the wave holds exactly row(k): dilate the three row masks once, in
       // scalar registers, and test the lane's column bit
       const int r = __builtin_amdgcn_readfirstlane(row(k));
-      uint64_t x = rm[r];
-      if (r > 0) x |= rm[r - 1];
-      if (r < H - 1) x |= rm[r + 1];
+      uint64_t x = rm[r - 1] | rm[r] | rm[r + 1];
       x = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
       const uint64_t d = x | (x << 1) | (x >> 1);
@@ -343,8 +348,8 @@ struct FullWorld {
       for (int k = 0; k < CPT; ++k) {
         const int i = cell(k), ibl = nb(k, 1, go), iar = nb(k, -1, -go);
         const uint32_t a = s.a[i], bl = s.a[ibl], ar = s.a[iar];
-        const bool elem = fid(a) == kSand || fid(a) == kDust;
-        const bool elem_ar = fid(ar) == kSand || fid(ar) == kDust;
+        const bool elem = in_set(bit(kSand) | bit(kDust), fid(a));
+        const bool elem_ar = in_set(bit(kSand) | bit(kDust), fid(ar));
         const bool ndg = !fdidg(a);
         const bool f_own = (s.rb[i] & 1u) == fl, f_ar = (s.rb[iar] & 1u) == fl;
         const bool mv = elem & !fdidg(bl) & f_own & (dens_i(a) > dens_i(bl)) & (bool)fgrav(bl) & ndg;
@@ -459,10 +464,10 @@ struct FullWorld {
     asm volatile("; ICE_BEGIN");
 #endif
     fence_idx();
-    uint64_t* melt = s.rowm[0];  // empty | fire | lava | water
+    uint64_t* melt = rmask(0);  // empty | fire | lava | water
     row_masks(melt, [&](int k) {
       const uint32_t x = fid(s.a[cell(k)]);
-      return x == kEmpty || x == kFire || x == kLava || x == kWater;
+      return in_set(bit(kEmpty) | bit(kFire) | bit(kLava) | bit(kWater), x);
     });
     sync();
 #pragma unroll
@@ -476,7 +481,7 @@ struct FullWorld {
 
   __device__ __forceinline__ void water() const {
     fence_idx();
-    uint64_t* ice = s.rowm[0];
+    uint64_t* ice = rmask(0);
     row_masks(ice, [&](int k) { return fid(s.a[cell(k)]) == kIce; });
     sync();
 #pragma unroll
@@ -488,10 +493,9 @@ struct FullWorld {
     sync();
   }
 
-  __device__ static __forceinline__ bool burnable(uint32_t x) {
-    return x == kWood || x == kPlant || x == kGas || x == kDust || x == kFish || x == kBird || x == kKangaroo ||
-           x == kMole || x == kLemming;
-  }
+  static constexpr uint32_t kBurnable = bit(kWood) | bit(kPlant) | bit(kGas) | bit(kDust) | bit(kFish) | bit(kBird) |
+                                        bit(kKangaroo) | bit(kMole) | bit(kLemming);
+  __device__ static __forceinline__ bool burnable(uint32_t x) { return in_set(kBurnable, x); }
 
   // BehaviorFire (sim.py:700-790).  The "is there X in my 3x3" and "how
   // many burnable cells in my 3x3" questions are answered from per-row
@@ -503,14 +507,14 @@ struct FullWorld {
 #endif
     static_assert(CPT <= 8, "conversion codes packed 8 bits per cell");
     fence_idx();
-    uint64_t* hotm = s.rowm[0];   // fire | lava before the burn
-    uint64_t* burnm = s.rowm[1];  // burnable cells after the burn
-    uint64_t* srcm = s.rowm[2];   // fire spread sources
+    uint64_t* hotm = rmask(0);   // fire | lava before the burn
+    uint64_t* burnm = rmask(1);  // burnable cells after the burn
+    uint64_t* srcm = rmask(2);   // fire spread sources
     uint32_t flb = 0;             // bit k: this cell was fire or lava before the burn
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const uint32_t id = fid(s.a[cell(k)]);
-      flb |= (id == kFire || id == kLava) ? 1u << k : 0u;
+      flb |= in_set(bit(kFire) | bit(kLava), id) ? 1u << k : 0u;
     }
     row_masks(hotm, [&](int k) { return ((flb >> k) & 1u) != 0u; });
     sync();
@@ -523,9 +527,11 @@ struct FullWorld {
       const uint32_t id = fid(s.a[i]);
       const bool nr = any3x3(hotm, k);
       const bool p005 = ri_lt(k, kRi005), p02 = ri_lt(k, kRi02);
-      const bool cand = (id == kWood && p005) | (id == kPlant && p02) | (id == kGas && p02) | (id == kDust) |
-                        (id == kBird && p005) |
-                        ((id == kFish || id == kLemming || id == kKangaroo || id == kMole) && p02);
+      // burn candidates: wood, bird at ri < 0.05; plant, gas and the animals at
+      // ri < 0.2; dust always
+      constexpr uint32_t k005 = bit(kWood) | bit(kBird);
+      constexpr uint32_t k02 = bit(kPlant) | bit(kGas) | bit(kFish) | bit(kLemming) | bit(kKangaroo) | bit(kMole);
+      const bool cand = (in_set(k005, id) & p005) | (in_set(k02, id) & p02) | (id == kDust);
       const bool burn = cand & nr, burn_ice = (id == kIce) & p02 & nr;
       s.f2[i] = (uint8_t)((burn ? 1 : 0) | (((id == kDust) & nr) ? 2 : 0));
       conv |= (Codes)(burn ? kFire + 1u : (burn_ice ? kWater + 1u : 0u)) << (8 * k);
@@ -599,12 +605,12 @@ struct FullWorld {
     asm volatile("; PLANT_BEGIN");
 #endif
     fence_idx();
-    uint64_t* plm = s.rowm[0];  // plant
-    uint64_t* iwm = s.rowm[1];  // ice | wood
+    uint64_t* plm = rmask(0);  // plant
+    uint64_t* iwm = rmask(1);  // ice | wood
     row_masks(plm, [&](int k) { return fid(s.a[cell(k)]) == kPlant; });
     row_masks(iwm, [&](int k) {
       const uint32_t x = fid(s.a[cell(k)]);
-      return x == kIce || x == kWood;
+      return in_set(bit(kIce) | bit(kWood), x);
     });
     sync();
 #pragma unroll
