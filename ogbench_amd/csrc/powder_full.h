@@ -788,12 +788,16 @@ struct FullWorld {
 
   // The value at column col - 1 / col + 1 of the same row (a wave holds whole
   // rows: DPP wave_shr / wave_shl by one lane), +0 outside the world.
+  // At W = 64 the wave is the row: the shift's out-of-range lane (column 0 /
+  // 63) already reads +0 (bound_ctrl), so no select is needed.
   __device__ __forceinline__ float col_prev(float x) const {
     const float y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x138, 0xF, 0xF, true));
+    if constexpr (W == 64) return y;
     return col == 0 ? 0.0f : y;
   }
   __device__ __forceinline__ float col_next(float x) const {
     const float y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xF, 0xF, true));
+    if constexpr (W == 64) return y;
     return col == W - 1 ? 0.0f : y;
   }
 
