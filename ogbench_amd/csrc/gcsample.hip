@@ -219,11 +219,7 @@ __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int6
 // so in-lane calls would run kCalls dependent-free chains on two lanes; spread
 // over 2 * kCalls lanes each lane runs one.  Same counters and keys as the
 // in-lane form, so the words are identical.
-#ifndef OGBX_GC_NOSPREAD
 constexpr bool kGcSpread = true;
-#else
-constexpr bool kGcSpread = false;
-#endif
 // Every lane of a wave that has a call computes one (lanes past the last call
 // repeat one and store nothing): gfx950 issues a dependent integer chain about
 // twice as slowly with <= 16 active lanes, and a B = 1,024 tile
@@ -245,9 +241,6 @@ __device__ inline void tile_philox(uint4 (*wb)[kGcMaxTile], int calls, int n_her
 // 128-B lines where one sample's output rows meet the next are merged in
 // that XCD's L2 instead of being written back twice.
 __device__ inline int64_t xcd_tile() {
-#ifdef OGBX_GC_NO_XCD
-  return blockIdx.x;
-#endif
   const int64_t b = blockIdx.x, nb = gridDim.x;
   const int64_t per = nb >> 3, rem = nb & 7, x = b & 7;
   return x * per + (x < rem ? x : rem) + (b >> 3);

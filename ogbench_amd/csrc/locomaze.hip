@@ -27,13 +27,6 @@
 #include "point_physics.h"
 #include "point_contact.h"
 
-// Contact step: the active-set form (point_contact.h) by default;
-// -DOGBX_PHYS_V1 selects the evaluate-and-step form of point_physics.h (A/B only).
-#ifdef OGBX_PHYS_V1
-#define OGBX_POINT_STEP point_step
-#else
-#define OGBX_POINT_STEP point_step_as
-#endif
 
 namespace ogbx {
 
@@ -86,11 +79,7 @@ namespace ogbx {
 // The contact model is the same for every maze (P.pm == kPointModel, checked at
 // create): the step kernels use the compile-time copy so its ~30 constants fold
 // into the instructions instead of living in (spilled) SGPRs.
-#ifdef OGBX_RUNTIME_MODEL
-#define OGBX_POINT_MODEL(pm, P) const PointModel pm = (P).pm
-#else
 #define OGBX_POINT_MODEL(pm, P) constexpr PointModel pm = kPointModel
-#endif
 
 __device__ inline void stage_wall(const MazeParams& P, uint8_t* wall_s) {
   for (int t = threadIdx.x; t < P.H * P.W; t += blockDim.x) wall_s[t] = P.wall[t];
@@ -314,7 +303,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     if (P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
     x = x + dx;
     y = y + dy;
-    OGBX_POINT_STEP(pm, nb_s, P.H, P.W, &x, &y);
+    point_step_as(pm, nb_s, P.H, P.W, &x, &y);
     if (!P.success_pre) succ = goal_reached(x, y, gx, gy, P.goal_tol);
     const double ox = x, oy = y;  // ob is taken before a teleport (maze.py:437-451)
     if (P.n_tp_in > 0) {
@@ -422,7 +411,7 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
   const MazeParams& P = *Pp;
   x = x + ax;
   y = y + ay;
-  int c = OGBX_POINT_STEP(pm, nb_s, P.H, P.W, &x, &y);
+  int c = point_step_as(pm, nb_s, P.H, P.W, &x, &y);
   qpos_out[2 * i] = x;
   qpos_out[2 * i + 1] = y;
   if (contact_out) contact_out[i] = (uint8_t)c;
@@ -813,17 +802,6 @@ ogbx_status ogbx_maze_set_envs_per_wave(ogbx_maze_t e, int32_t epw) {
   e->epw = epw;
   return OGBX_OK;
 }
-
-#ifdef OGBX_PHYS_STAMPS
-// Diagnostic build only: read and clear the per-wave stamp sums [4096][4].
-ogbx_status ogbx_diag_phys_stamps(unsigned long long* out) {
-  OGBX_HIP(hipDeviceSynchronize());
-  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phys_stamps), 4096 * 4 * sizeof(unsigned long long)));
-  static unsigned long long z[4096 * 4];
-  OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_phys_stamps), z, sizeof(z)));
-  return OGBX_OK;
-}
-#endif
 
 #ifdef OGBX_WAVE_STAMPS
 // Diagnostic build only: per-wave (start, end) wall clock (s_memrealtime,

@@ -45,12 +45,8 @@ namespace ogbx {
 // allocate in the cache (measured: easy 25.8 -> 23.5 us per launch).
 typedef unsigned int pw_u32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void pw_nt_store16(uint4* d, const uint4& v) {
-#ifdef OGBX_PW_CACHED_OBS  // A/B: plain stores
-  *d = v;
-#else
   pw_u32x4v x = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(x, reinterpret_cast<pw_u32x4v*>(d));
-#endif
 }
 
 constexpr int kPwMaxSeq = 256;
@@ -562,14 +558,9 @@ __global__ void __launch_bounds__(256) pw_forward_kernel(const PowderParams* __r
 // per thread).  A 64x64 world holds 78 KB of LDS and 8 waves, so two worlds
 // share a CU and one world's barrier waits overlap the other's work: 0.280 ->
 // 0.220 ms per medium step against 1024 threads (one world per CU).
-#ifndef OGBX_PWF_NT64
-#define OGBX_PWF_NT64 512  // threads per 64x64 world
-#endif
 template <int WS>
-constexpr int pwf_nt() { return WS == 64 ? OGBX_PWF_NT64 : 256; }
-#ifndef OGBX_PWF_WAVES
-#define OGBX_PWF_WAVES 4  // waves per SIMD the register budget is sized for
-#endif
+constexpr int pwf_nt() { return WS == 64 ? 512 : 256; }  // threads per world
+constexpr int kPwfWaves = 4;  // waves per SIMD the register budget is sized for
 template <int WS>
 using FW = FullWorld<WS, pwf_nt<WS>()>;
 
@@ -613,7 +604,7 @@ __device__ __forceinline__ void pwf_reset_op(const FW<WS>& fw, const PowderParam
 }
 
 template <int WS>
-__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(OGBX_PWF_WAVES))) pwf_reset_kernel(const PowderParams* __restrict__ Pp, PowderState S,
+__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(kPwfWaves))) pwf_reset_kernel(const PowderParams* __restrict__ Pp, PowderState S,
                                                         const int32_t* __restrict__ task_id,
                                                         const uint8_t* __restrict__ mask,
                                                         const int32_t* __restrict__ reset_action,
@@ -657,15 +648,9 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
 
 // k_steps env steps; rand: [k, N, 3, H, W] injected fields for the forward of
 // each third step, or NULL = Philox (auto-resets always use Philox).
-#ifdef OGBX_PWF_STAMPS
-// Diagnostic build only: per-env wall clock (s_memrealtime, 100 MHz) at entry,
-// after the state load, before the observation and at exit of the last
-// pwf_step_kernel launch.
-__device__ unsigned long long g_pwf_stamps[4096 * 4];
-#endif
 
 template <int WS>
-__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(OGBX_PWF_WAVES))) pwf_step_kernel(
+__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(kPwfWaves))) pwf_step_kernel(
     const PowderParams* __restrict__ Pp, PowderState S, int64_t n, const int32_t* __restrict__ action,
     const int32_t* __restrict__ draws, const float* __restrict__ rand, int32_t k_steps, uint8_t* __restrict__ obs,
     float* __restrict__ reward, uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated,
@@ -680,9 +665,6 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   pwf_tables(sh, Pp);
   const int grid = Pp->grid, brush = Pp->brush, xy = Pp->xy_size, ne = Pp->num_elems;
   const int max_steps = Pp->max_steps;
-#ifdef OGBX_PWF_STAMPS
-  const unsigned long long ts0 = wall_clock64();
-#endif
   fw.load(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) sh.g[fw.cell(k)] = S.goal_env[(size_t)e * C + fw.cell(k)];
@@ -693,10 +675,6 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   const int tol = Pp->tol_task[(task >= 1 && task <= Pp->num_tasks ? task : 1) - 1];
   bool dirty = false, goal_dirty = false;
   __syncthreads();
-#ifdef OGBX_PWF_STAMPS
-  const unsigned long long ts1 = wall_clock64();
-  unsigned long long ts2 = ts1;
-#endif
   const int len = Pp->seq_len[task - 1];
   for (int k = 0; k < k_steps; ++k) {
     fw.fence_idx();
@@ -762,21 +740,9 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     }
     ctrl = stage | (elem << 2) | (x << 8) | (ctrl & (255 << 16)) | (succ ? kCtrlSuccess : 0);
     const uint32_t acol = sh.lut[sh.elem_ids[elem & 7] & 31];
-#ifdef OGBX_PWF_STAMPS
-    ts2 = wall_clock64();
-#endif
     fw.observe(obs + (size_t)o * C * 6, stage, acol, x * grid, brush);
   }
   if (dirty) fw.store(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
-#ifdef OGBX_PWF_STAMPS
-  if (threadIdx.x == 0 && e < 4096) {
-    const unsigned long long ts3 = wall_clock64();
-    g_pwf_stamps[4 * e + 0] = ts0;
-    g_pwf_stamps[4 * e + 1] = ts1;
-    g_pwf_stamps[4 * e + 2] = ts2;
-    g_pwf_stamps[4 * e + 3] = ts3;
-  }
-#endif
   if (goal_dirty) {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
@@ -881,7 +847,7 @@ __global__ void __launch_bounds__(256) pwf_light_step_kernel(
 // float32 layout (tests / drop-in): rand [steps, n, 3, H, W] or NULL (Philox
 // keyed by the env seed); optional render of the result (n, H, W, 3).
 template <int WS>
-__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(OGBX_PWF_WAVES))) pwf_forward_kernel(const PowderParams* __restrict__ Pp,
+__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(kPwfWaves))) pwf_forward_kernel(const PowderParams* __restrict__ Pp,
                                                           const float* __restrict__ in, int64_t n, int32_t steps,
                                                           const float* __restrict__ rand, float* __restrict__ out,
                                                           uint8_t* __restrict__ rgb, uint32_t r0, uint32_t r1) {
@@ -1138,13 +1104,6 @@ ogbx_status ogbx_powder_task_table(int32_t num_elems, int32_t task_id, int32_t* 
   return OGBX_OK;
 }
 
-#ifdef OGBX_PWF_STAMPS
-extern "C" ogbx_status ogbx_diag_pwf_stamps(unsigned long long* out) {
-  OGBX_HIP(hipDeviceSynchronize());
-  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(ogbx::g_pwf_stamps), 4096 * 4 * sizeof(unsigned long long)));
-  return OGBX_OK;
-}
-#endif
 
 #ifdef OGBX_PWF_RULE_STAMPS
 extern "C" ogbx_status ogbx_diag_pwf_rules(unsigned long long* out) {

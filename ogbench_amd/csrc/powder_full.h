@@ -316,9 +316,6 @@ struct FullWorld {
     return (dens_i(b) < dens_i(a)) & (bool)fgrav(a) & (bool)fgrav(b);
   }
   __device__ __forceinline__ void gravity() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; GRAV_BEGIN");
-#endif
     fence_idx();
     Moves mv;
 #pragma unroll
@@ -335,9 +332,6 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void sand() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; SAND_BEGIN");
-#endif
     fence_idx();
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
@@ -413,9 +407,6 @@ struct FullWorld {
   // real(back); the new momentum is per position.  Rows without an element
   // that can start a move are skipped wave-uniformly.
   __device__ __forceinline__ void fluid() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; FLUID_BEGIN");
-#endif
     fence_idx();
 #pragma unroll 1
     for (int k = 0; k < CPT; ++k) {  // rows are independent: rolled, few live registers
@@ -460,9 +451,6 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void ice() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; ICE_BEGIN");
-#endif
     fence_idx();
     uint64_t* melt = rmask(0);  // empty | fire | lava | water
     row_masks(melt, [&](int k) {
@@ -502,9 +490,6 @@ struct FullWorld {
   // bitmasks (row_masks): fire|lava before the burn, the burnable cells after
   // it, and the spread sources.
   __device__ __forceinline__ void fire() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; FIRE_BEGIN");
-#endif
     static_assert(CPT <= 8, "conversion codes packed 8 bits per cell");
     fence_idx();
     uint64_t* hotm = rmask(0);   // fire | lava before the burn
@@ -601,9 +586,6 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void plant() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; PLANT_BEGIN");
-#endif
     fence_idx();
     uint64_t* plm = rmask(0);  // plant
     uint64_t* iwm = rmask(1);  // ice | wood
@@ -636,17 +618,9 @@ struct FullWorld {
   }
 
   __device__ __forceinline__ void velocity() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; VEL_BEGIN");
-#endif
     fence_idx();
-#ifdef OGBX_PWF_VEL  // timing ablation: bit 0 = swap passes, bit 1 = decay + blur
-    constexpr int kVelParts = OGBX_PWF_VEL;
-#else
-    constexpr int kVelParts = 3;
-#endif
 #pragma unroll 1
-    for (int pass = 0; pass < ((kVelParts & 1) ? 2 : 0); ++pass) {
+    for (int pass = 0; pass < 2; ++pass) {
       fence_idx();
       // f2 = angle bin of cells that may move (mag above the pass threshold, not
       // wall), 0xFF otherwise; sw = chosen swap direction (-1 none)
@@ -753,7 +727,6 @@ struct FullWorld {
     // 9) and takes the column neighbours' taps from the adjacent lanes with
     // DPP wave shifts (zero outside the row); the results stay in registers
     // until every thread has read the field.
-    if (!(kVelParts & 2)) return;
     const float w18 = 1.0f / 18.0f;
     fence_idx();
     float2 res[CPT];
@@ -919,12 +892,6 @@ struct FullWorld {
 
   // Goal mismatch count against s.g (powderworld_env.py:410-418); block total.
   __device__ __forceinline__ int errors() const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; ERR_BEGIN");
-#endif
-#ifdef OGBX_PWF_ABL_NOERR  // timing ablation
-    return 1 << 20;
-#endif
     fence_idx();
     int err = 0;
 #pragma unroll
@@ -952,12 +919,6 @@ struct FullWorld {
   // 16-byte stores.  rgb_only: 3 channels.
   __device__ __forceinline__ void observe(uint8_t* __restrict__ dst, int stage, uint32_t acol, int rx, int brush,
                                           bool rgb_only = false) const {
-#ifdef OGBX_ASM_MARKS
-    asm volatile("; OBS_BEGIN");
-#endif
-#ifdef OGBX_PWF_ABL_NOOBS  // timing ablation
-    return;
-#endif
     fence_idx();
     const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
     const uint32_t px = fr ? acol : 0u;
@@ -1043,12 +1004,7 @@ struct FullWorld {
 #else
   __device__ __forceinline__ void forward_masked(uint32_t P) const {
 #endif
-#ifdef OGBX_PWF_RULES  // ablation builds (scripts/build_pwf_variants.sh): run only the rules in the mask
-    constexpr uint32_t R = OGBX_PWF_RULES;
-#else
-    constexpr uint32_t R = ~0u;
-#endif
-    // R bits: 1 stone, 4 sand, 8 fluid, 16 ice, 32 water, 64 fire, 128 plant, 256 velocity
+    constexpr uint32_t R = ~0u;  // every rule (bits: 1 stone, 4 sand, 8 fluid, 16 ice, 32 water, 64 fire, 128 plant, 256 velocity)
     if ((R & 1) && (P & bit(kStone))) stone();
     OGBX_RS(1);
     gravity();

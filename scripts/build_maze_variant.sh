@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build _ab/libogbx_<name>.so: libogbx with $SRC.hip (default locomaze) compiled under
+# Build _abx/libogbx_<name>.so: libogbx with $SRC.hip (default locomaze) compiled under
 # extra flags (the other objects from build/obj, built by `make`).  Run here.
 # usage: scripts/build_maze_variant.sh <name> [-DFLAG ...]
 set -eu
@@ -12,6 +12,6 @@ mkdir -p build/var
 SRC=${SRC:-locomaze}
 $H $F "$@" -c ogbench_amd/csrc/$SRC.hip -o build/var/${SRC}_$name.o
 objs=$(ls build/obj/*.o | grep -v "/$SRC\.o" | tr '\n' ' ')
-mkdir -p _ab
-$H --offload-arch=gfx950 -shared -fPIC -o _ab/libogbx_$name.so $objs build/var/${SRC}_$name.o
-echo _ab/libogbx_$name.so
+mkdir -p _abx
+$H --offload-arch=gfx950 -shared -fPIC -o _abx/libogbx_$name.so $objs build/var/${SRC}_$name.o
+echo _abx/libogbx_$name.so

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build _ab/libogbx_pwf_<name>.so: libogbx with powder.hip compiled under
+# Build _abx/libogbx_pwf_<name>.so: libogbx with powder.hip compiled under
 # extra flags (the other objects from build/obj, built by `make`).  Run here.
 # usage: scripts/build_pwf_variant.sh <name> [-DOGBX_PWF_RULES=<mask> ...]
 set -eu
@@ -11,6 +11,6 @@ F="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -w"
 mkdir -p build/var
 $H $F "$@" -c ogbench_amd/csrc/powder.hip -o build/var/powder_$name.o
 objs=$(ls build/obj/*.o | grep -v '/powder' | tr '\n' ' ')
-mkdir -p _ab
-$H --offload-arch=gfx950 -shared -fPIC -o _ab/libogbx_pwf_$name.so $objs build/var/powder_$name.o
-echo _ab/libogbx_pwf_$name.so
+mkdir -p _abx
+$H --offload-arch=gfx950 -shared -fPIC -o _abx/libogbx_pwf_$name.so $objs build/var/powder_$name.o
+echo _abx/libogbx_pwf_$name.so

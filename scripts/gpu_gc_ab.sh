@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gc_gpu.py tests/test_hgc_gpu.py -m gpu -x -q --timeout 200 \
   --timeout-method thread > gpurun_out/gc_pytest.log 2>&1
 rc=$?; tail -2 gpurun_out/gc_pytest.log; [ $rc -eq 0 ] || exit $rc
-LIBS=${LIBS:-"ogbench_amd/libogbx.so $(ls _ab/libogbx_*.so 2>/dev/null | tr '\n' ' ')"}
+LIBS=${LIBS:-"ogbench_amd/libogbx.so $(ls _abx/libogbx_*.so 2>/dev/null | tr '\n' ' ')"}
 for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in $LIBS; do
     for wl in gcsample hgcsample; do

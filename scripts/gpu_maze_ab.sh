@@ -1,12 +1,12 @@
 #!/bin/bash
 # A/B of locomaze builds (GPU box): the timed pointmaze bench at N = 65,536 and
 # 8,192 under each library in $LIBS (default: the in-tree libogbx.so and every
-# _ab/libogbx_*.so), alternating, $ROUNDS rounds.
+# _abx/libogbx_*.so), alternating, $ROUNDS rounds.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-LIBS=${LIBS:-"ogbench_amd/libogbx.so $(ls _ab/libogbx_*.so 2>/dev/null | tr '\n' ' ')"}
+LIBS=${LIBS:-"ogbench_amd/libogbx.so $(ls _abx/libogbx_*.so 2>/dev/null | tr '\n' ' ')"}
 for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in $LIBS; do
     for N in ${NS:-65536 8192}; do

@@ -1,11 +1,11 @@
 #!/bin/bash
 # A/B of powder builds (GPU box): the powder / powder-medium bench (timed step
-# only) under the in-tree library and each _ab/libogbx_pwf_*.so,
+# only) under the in-tree library and each _abx/libogbx_pwf_*.so,
 # alternating, $ROUNDS rounds.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-LIBS=${LIBS:-"ogbench_amd/libogbx.so $(ls _ab/libogbx_pwf_*.so 2>/dev/null | tr '\n' ' ')"}
+LIBS=${LIBS:-"ogbench_amd/libogbx.so $(ls _abx/libogbx_pwf_*.so 2>/dev/null | tr '\n' ' ')"}
 for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in $LIBS; do
     for wl in ${WLS:-powder powder-medium}; do

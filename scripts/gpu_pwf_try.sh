@@ -1,6 +1,6 @@
 #!/bin/bash
 # Powder medium/hard A/B (GPU box): parity tests + bench for the in-tree build,
-# then for each _ab/libogbx_pwf_*.so variant (parity + bench).  Tuning only.
+# then for each _abx/libogbx_pwf_*.so variant (parity + bench).  Tuning only.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -16,7 +16,7 @@ one() {  # $1 = tag, OGBX_LIB from the env
   done
 }
 one intree || exit $?
-for f in _ab/libogbx_pwf_*.so; do
+for f in _abx/libogbx_pwf_*.so; do
   [ -f "$f" ] || continue
   t=$(basename $f .so); OGBX_LIB=$f one ${t#libogbx_pwf_} || exit $?
 done

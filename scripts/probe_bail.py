@@ -2,7 +2,7 @@
 (point_contact.h point_step_as; counter 14 = waves that redo the step).
 Inputs: the near-wall random states of tests/test_locomaze_gpu.py and the
 bench's warmed-up pointmaze-large states.
-Run with OGBX_LIB=_ab/libogbx_stats.so (scripts/build_maze_variant.sh stats -DOGBX_PHYS_STATS)."""
+Run with OGBX_LIB=_abx/libogbx_stats.so (scripts/build_maze_variant.sh stats -DOGBX_PHYS_STATS)."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, ogbench_amd

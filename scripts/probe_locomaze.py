@@ -1,6 +1,6 @@
 """Perf probe: physics-kernel time vs contact fraction (separates launch cost
 from contact compute).  Not part of the bench contract.  OGBX_LIB selects a
-diagnostic build (any libogbx.so variant under _ab/)."""
+diagnostic build (any libogbx.so variant under _abx/)."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, ogbench_amd

@@ -1,7 +1,7 @@
 """Diagnostic: shader-clock cycles per rule of the powder forward (per env and
 forward, averaged) in the powder-medium bench setting, from the rule-stamp
 build: SRC=powder scripts/build_maze_variant.sh pwfrs -DOGBX_PWF_RULE_STAMPS,
-then OGBX_LIB=_ab/libogbx_pwfrs.so python scripts/probe_pwf_rules.py [medium|hard]."""
+then OGBX_LIB=_abx/libogbx_pwfrs.so python scripts/probe_pwf_rules.py [medium|hard]."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, ogbench_amd

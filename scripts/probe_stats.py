@@ -1,5 +1,5 @@
 """Diagnostic: physics path counters on realistic states (a warmed-up
-pointmaze-large rollout).  Run with OGBX_LIB=_ab/libogbx_stats.so.
+pointmaze-large rollout).  Run with OGBX_LIB=_abx/libogbx_stats.so.
 Counters: [0..3] lane-stages with n contacts, 4 Newton iterations (lanes),
 5 Armijo fallbacks, 6 contact steps (lanes), 8 wave-stages in Newton mode,
 9 wave-stages on the contact path, 10 wave-stages with a transition-band gain,

@@ -1,6 +1,6 @@
 """Diagnostic: per-wave duration distribution of one maze_step_kernel launch in
 the bench setting (pointmaze-large, N envs, after `warm` auto-reset steps).
-Run with OGBX_LIB=_ab/libogbx_<v>.so built with -DOGBX_WAVE_STAMPS
+Run with OGBX_LIB=_abx/libogbx_<v>.so built with -DOGBX_WAVE_STAMPS
 (scripts/build_maze_variant.sh <v> -DOGBX_WAVE_STAMPS [...])."""
 import ctypes, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
