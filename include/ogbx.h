@@ -46,6 +46,16 @@ typedef enum {
 const char* ogbx_last_error(void);
 /* OGBX_ABI_VERSION of the loaded library. */
 int32_t ogbx_abi_version(void);
+
+/* Version of the Philox random streams: which counter words feed which draw.
+ * The same seed reproduces a run only between libraries with the same stream
+ * version (tests/test_stream_pin_gpu.py pins the outputs of every Philox
+ * consumer at this version).  History: 1 = rounds 1-2; 2 = powderworld
+ * medium/hard rand fields from three Philox calls per group of four cells
+ * (all 12 words used), where version 1 took one call per cell. */
+#define OGBX_STREAM_VERSION 2
+/* OGBX_STREAM_VERSION of the loaded library. */
+int32_t ogbx_stream_version(void);
 /* Name of the GPU architecture the library was built for ("gfx950"). */
 const char* ogbx_build_arch(void);
 

@@ -60,6 +60,7 @@ class PowderOpts(ctypes.Structure):
 _SIGNATURES = {
     'ogbx_last_error': (c_char_p, []),
     'ogbx_abi_version': (c_int32, []),
+    'ogbx_stream_version': (c_int32, []),
     'ogbx_build_arch': (c_char_p, []),
     # locomaze
     'ogbx_maze_create': (c_int32, [c_char_p, c_int64, c_int32, P(MazeOpts), P(c_void_p)]),

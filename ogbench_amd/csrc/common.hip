@@ -44,6 +44,7 @@ extern "C" {
 const char* ogbx_last_error(void) { return ogbx::g_last_error.c_str(); }
 
 int32_t ogbx_abi_version(void) { return OGBX_ABI_VERSION; }
+int32_t ogbx_stream_version(void) { return OGBX_STREAM_VERSION; }
 
 const char* ogbx_build_arch(void) { return "gfx950"; }
 

@@ -234,7 +234,9 @@ class GCDataset:
     """Goal-conditioned sampler (reference: datasets.py:149-366).
 
     config keys read (as the reference): discount, value_/actor_ p_curgoal,
-    p_trajgoal, p_randomgoal, geom_sample, gc_negative, p_aug, frame_stack.
+    p_trajgoal, p_randomgoal, geom_sample, gc_negative, p_aug, frame_stack;
+    and one of this sampler's own: row_record (default True; False skips the
+    interleaved copy of the small columns, ``_row_record``).
     """
 
     def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None, _plain=False):
@@ -282,7 +284,8 @@ class GCDataset:
                              self.valid_traj_end.data_ptr() if valid is not None else None,
                              self.valid_pairs.data_ptr() if valid is not None else None, *self.period)
         self._valid = valid
-        self._record, self._rec_off = self._row_record(dataset)
+        self._plain = _plain
+        self._record, self._rec_off, self._rec_stride, self._rec_src = self._row_record(dataset)
 
         def thresh(p_traj, p_cur):
             return p_traj / (1.0 - p_cur) if p_cur != 1.0 else 0.0  # datasets.py:321
@@ -296,37 +299,76 @@ class GCDataset:
         )
         self._seed = int(seed) if seed is not None else None
         self._calls = 0
-        self._plain = _plain
         self._out_cache = {}
 
     # ---------------------------------------------------------------- helpers
-    _RECORD_BYTES = 128  # one L2 line
+    _RECORD_MAX = 128  # one L2 line
 
     def _row_record(self, ds):
         """The sampler's own interleaved copy of the dataset's small columns
         (every key but the goal sources whose row is 4-byte granular, packed in
         key order while they fit one 128-B line per row, e.g. actions 84 +
         terminals 4 + valids 4 of the humanoid layout): a sample's rows of them
-        then come from one line of HBM instead of one line per column.  The
+        then come from one line of HBM instead of one line per column.  The row
+        stride is the power of two (16..128 B) at or above the packed bytes, so
+        a row never straddles a line and the copy costs no more than it must
+        (pointmaze: actions 8 + terminals 4 + valids 4 = 16 B per row).  The
         dataset's own tensors (and the returned batch) keep the reference
-        shapes.  None when fewer than two columns fit."""
+        shapes.  Not built for the plain Dataset.sample sampler, with fewer
+        than two packable columns, or with config['row_record'] = False.
+
+        The reference freezes its dataset (Dataset.create sets the arrays
+        read-only, impls/utils/datasets.py:45-56); torch tensors cannot be made
+        read-only, so sample() checks the packed columns' version counters
+        and identities and refreshes the copy if one was modified
+        (``_refresh_record``)."""
         torch = _torch()
+        if self._plain or not self.config.get('row_record', True):
+            return None, {}, 0, ()
         goal_srcs = {'observations', 'oracle_reps'}
         off, picks = 0, []
         for k, v in ds.items():
             if k in goal_srcs:
                 continue
             rb = (v[0].numel() if v.dim() > 1 else 1) * v.element_size()
-            if rb % 4 or off + rb > self._RECORD_BYTES:
+            if rb % 4 or off + rb > self._RECORD_MAX:
                 continue
             picks.append((k, off, rb))
             off += rb
         if len(picks) < 2:
-            return None, {}
-        rec = torch.zeros(self.size, self._RECORD_BYTES, dtype=torch.uint8, device=self.device)
-        for k, o, rb in picks:
-            rec[:, o:o + rb] = ds[k].reshape(self.size, -1).contiguous().view(torch.uint8)
-        return rec, {k: o for k, o, _ in picks}
+            return None, {}, 0, ()
+        stride = 16
+        while stride < off:
+            stride *= 2
+        rec = torch.zeros(self.size, stride, dtype=torch.uint8, device=self.device)
+        src = tuple((k, ds[k], o, rb) for k, o, rb in picks)
+        self._fill_record(rec, src)
+        return rec, {k: o for k, o, _ in picks}, stride, tuple((k, t, o, rb, t._version) for k, t, o, rb in src)
+
+    def _fill_record(self, rec, src):
+        torch = _torch()
+        for k, t, o, rb in src:
+            rec[:, o:o + rb] = t.reshape(self.size, -1).contiguous().view(torch.uint8)
+
+    def _refresh_record(self):
+        """Re-pack the row record if a packed column was modified in place or
+        replaced since it was built (same layout, same record buffer: the
+        cached column descriptors stay valid, except on replacement)."""
+        ds = self.dataset
+        stale = False
+        for k, t, _, _, ver in self._rec_src:
+            cur = ds.get(k)
+            if cur is not t:
+                if cur is None or cur.shape != t.shape or cur.dtype != t.dtype:
+                    raise ValueError(f'dataset column {k!r} changed shape or dtype after the sampler was built')
+                self._out_cache.clear()  # the batch descriptors hold the old column pointers
+                stale = True
+            elif t._version != ver:
+                stale = True
+        if stale:
+            src = tuple((k, ds[k], o, rb) for k, _, o, rb, _ in self._rec_src)
+            self._fill_record(self._record, src)
+            self._rec_src = tuple((k, t, o, rb, t._version) for k, t, o, rb in src)
 
     def _column(self, src_key, dst, select):
         """Descriptor of one gathered column (from the row record when the key
@@ -335,7 +377,7 @@ class GCDataset:
         row_bytes = src[0].numel() * src.element_size() if src.dim() > 1 else src.element_size()
         o = self._rec_off.get(src_key)
         if o is not None:
-            return GcColumn(self._record.data_ptr() + o, dst.data_ptr(), row_bytes, select, self._RECORD_BYTES)
+            return GcColumn(self._record.data_ptr() + o, dst.data_ptr(), row_bytes, select, self._rec_stride)
         return GcColumn(src.data_ptr(), dst.data_ptr(), row_bytes, select, 0)
 
     def _p_aug_draw(self, out, evaluation):
@@ -391,6 +433,8 @@ class GCDataset:
         torch = _torch()
         total = int(batch_size) * int(num_batches)
         plain_call = idxs is None and not draws and not record_draws and _keys is None
+        if self._rec_src:
+            self._refresh_record()
         if out is not None and plain_call:
             hit = self._out_cache.get(id(out))
             if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
@@ -606,6 +650,8 @@ class HGCDataset(GCDataset):
         torch = _torch()
         total = int(batch_size) * int(num_batches)
         plain_call = idxs is None and not draws and not record_draws
+        if self._rec_src:
+            self._refresh_record()
         hit = self._out_cache.get(id(out)) if (out is not None and plain_call) else None
         if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
             _, _, col_arr, ncols, outs, _ = hit

@@ -22,6 +22,7 @@ Differences that follow from batching (documented in DESIGN.md):
 from __future__ import annotations
 
 import re
+import warnings
 
 import numpy as np
 
@@ -428,6 +429,14 @@ class MazeEnv:
             if gs is not None:
                 gs = torch.as_tensor(gs).to(self.device, torch.float64).contiguous()
                 assert gs.shape == (self.num_envs, 29), 'goal_states must be [num_envs, 29] (qpos, qvel)'
+            elif not self._use_oracle_rep and not getattr(self, '_warned_goal_states', False):
+                # the reference's goal observation is the body state after 5
+                # random-action physics steps (maze.py:408-418) -- the caller's
+                # physics; without it the unstepped reset_model state stands in
+                self._warned_goal_states = True
+                warnings.warn('antmaze reset without options["goal_states"]: info["goal"] is the unstepped '
+                              'reset_model pose, not the reference goal observation (pass the body state your '
+                              'physics reached after the goal reset, or use_oracle_rep=True)', stacklevel=2)
             gob = None if self._use_oracle_rep else self._goal_ob
             _lib.check(
                 self._L.ogbx_antmaze_reset(self._h, _lib.ptr(task_t), _lib.ptr(task_xy), _lib.ptr(m),
@@ -514,10 +523,11 @@ class MazeEnv:
         # Per-call host cost matters here (a 16k-env launch is ~5 us).  Fast
         # path: a (qpos, qvel) pair seen before -- the handle's own body_state()
         # views of an in-place engine, or a fixed ring of state buffers -- skips
-        # every layout check and pointer lookup: the pair's validated raw
-        # pointers are cached by tensor identity (the cache holds the tensors,
-        # so their ids stay unique while cached).  Anything else takes the
-        # checked path once and is cached.
+        # the dtype / device checks: the pair's validated raw pointers are
+        # cached by tensor identity (the cache holds the tensors, so their ids
+        # stay unique while cached) and a hit only re-reads the pointers, shapes
+        # and contiguity.  Anything else takes the checked path once and is
+        # cached (at most 8 pairs).
         rs = None
         if reset_states is not None:
             torch = _torch()
@@ -525,7 +535,12 @@ class MazeEnv:
             assert rs.shape == (self.num_envs, 29)
             rs = rs.data_ptr()
         hit = self._wrap_cache.get((id(qpos), id(qvel)))
-        if hit is not None and hit[0] is qpos and hit[1] is qvel:
+        # a hit is re-checked against the storage pointer, shape and layout it
+        # was validated with (set_ / resize_ / transpose_ / .data = ... change
+        # one of them); anything else revalidates
+        if (hit is not None and hit[0] is qpos and hit[1] is qvel and qpos.data_ptr() == hit[2]
+                and qvel.data_ptr() == hit[3] and qpos.shape == self._ant_qshape and qvel.shape == self._ant_vshape
+                and qpos.is_contiguous() and qvel.is_contiguous()):
             qp, vp = hit[2], hit[3]
         else:
             qp, vp = self._wrap_validate(qpos, qvel)
@@ -550,7 +565,7 @@ class MazeEnv:
             # referenced by the handle until the next such call, past the launch
             self._wrap_tmp = (q.contiguous(), v.contiguous())
             return self._wrap_tmp[0].data_ptr(), self._wrap_tmp[1].data_ptr()
-        if len(self._wrap_cache) >= 32:
+        if len(self._wrap_cache) >= 8:  # a small ring of engine buffers; bounds what the cache keeps alive
             self._wrap_cache.clear()
         qp, vp = q.data_ptr(), v.data_ptr()
         self._wrap_cache[(id(q), id(v))] = (q, v, qp, vp)

@@ -226,7 +226,7 @@ def main():
             ns = {'__name__': extra, '__file__': path}
             exec(compile(open(path).read(), path, 'exec'), ns)
             ns['main']()
-            for fn in ('main_hgc', 'main_relabel', 'main_names', 'main_full'):
+            for fn in ('main_hgc', 'main_periodic', 'main_relabel', 'main_names', 'main_full'):
                 if fn in ns:
                     ns[fn]()
 

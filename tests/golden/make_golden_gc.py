@@ -332,6 +332,93 @@ def main_hgc():
     print('hgc golden:', len(out), 'arrays')
 
 
+class PickRecorder(Recorder):
+    """Recorder whose randint calls (the sample and goal picks of
+    get_random_idxs, datasets.py:65-70) return the reference's own draws with
+    the first entries replaced by ``forced`` picks, logging what it returned."""
+
+    def __init__(self, forced):
+        super().__init__()
+        self.forced = np.asarray(forced, np.int64)
+
+    def __enter__(self):
+        super().__enter__()
+        inner = np.random.randint
+
+        def randint(*a, **k):
+            v = np.array(inner(*a, **k))
+            n = min(len(self.forced), v.size)
+            v[:n] = self.forced[:n]
+            self.log[-1] = ('randint', v.copy())
+            return v
+
+        np.random.randint = randint
+        return self
+
+
+def periodic_npz(path, rng, n_traj, L, ob_dim, act_dim):
+    """A raw .npz of n_traj equal trajectories of L rows (the OGBench layout:
+    every episode the same length, terminals = 1 at its last row)."""
+    R = n_traj * L
+    term = np.zeros(R, np.float32)
+    term[L - 1::L] = 1
+    np.savez(path, observations=rng.normal(size=(R, ob_dim)).astype(np.float32),
+             actions=rng.uniform(-1, 1, (R, act_dim)).astype(np.float32), terminals=term,
+             qpos=rng.uniform(-4, 40, (R, 2)).astype(np.float32))
+
+
+def main_periodic():
+    """Equal-length trajectories (30 x 50 rows; after the compact load the last
+    row of each is invalid: 49 picks per 50-row period, trajectory end at
+    offset 48).  libogbx samples such a buffer through its closed form
+    (ogbx_gc_buffer.period); these are the reference GCDataset / HGCDataset
+    outputs on it, with every pick, value-goal pick and actor-goal pick forced
+    to the period boundaries q*49 - 1, q*49 (and 0, npick - 1) in its first
+    entries and the reference's own draws elsewhere."""
+    utils, dsm, _ = reference_modules()
+    rng = np.random.RandomState(2024)
+    n_traj, L = 30, 50
+    out = {}
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, 'periodic.npz')
+        periodic_npz(path, rng, n_traj, L, ob_dim=5, act_dim=3)
+        raw = dict(np.load(path))
+        for k, v in raw.items():
+            out[f'raw_{k}'] = v
+        d = utils.load_dataset(path, compact_dataset=True, add_info=False)
+        npick = int((d['valids'] > 0).sum())
+        assert npick == n_traj * (L - 1)
+        q = np.arange(1, n_traj)
+        forced = np.concatenate([[0, npick - 1], q * (L - 1) - 1, q * (L - 1), q * (L - 1) + 1])
+        out['forced_picks'] = forced
+        B = 256
+        for cname, cfg in CONFIGS.items():
+            gc = dsm.GCDataset(dsm.Dataset.create(**d), dict(cfg))
+            tag = f'gc_{cname}'
+            np.random.seed(sum(map(ord, tag)) + 3)
+            with PickRecorder(forced) as rec:
+                batch = gc.sample(B)
+            for k, v in _draws_from_log(rec.log, B, cfg).items():
+                out[f'{tag}_draw_{k}'] = v
+            for k, v in batch.items():
+                out[f'{tag}_out_{k}'] = np.asarray(v)
+        for cname, cfg in HGC_CONFIGS.items():
+            hgc = dsm.HGCDataset(dsm.Dataset.create(**d), dict(cfg))
+            tag = f'hgc_{cname}'
+            np.random.seed(sum(map(ord, tag)) + 5)
+            with PickRecorder(forced) as rec:
+                batch = hgc.sample(B)
+            for k, v in hgc_draws_from_log(rec.log, B, cfg).items():
+                out[f'{tag}_draw_{k}'] = v
+            for k, v in batch.items():
+                out[f'{tag}_out_{k}'] = np.asarray(v)
+            out[f'{tag}_keys'] = np.array(list(batch.keys()))
+    np.savez_compressed(os.path.join(OUT, 'gc_periodic_golden.npz'), **out)
+    print('gc periodic golden:', len(out), 'arrays')
+
+
 def main_relabel():
     """relabel_dataset / add_oracle_reps (maze branch) of the reference
     ogbench/relabel_utils.py with a stand-in env (the attributes they read)."""
@@ -418,5 +505,6 @@ def main_names():
 if __name__ == '__main__':
     main()
     main_hgc()
+    main_periodic()
     main_relabel()
     main_names()

@@ -209,3 +209,47 @@ def test_wrap_step_cached_and_strided_inputs(gpu):
         a.wrap_step(qbuf[:, :14], vbuf)
     with pytest.raises(ValueError):
         a.wrap_step(qbuf.float(), vbuf)
+
+
+def test_wrap_step_cache_revalidates_mutated_tensors(gpu):
+    """a cached (qpos, qvel) pair whose storage or layout changes
+    in place (set_, resize_, transpose_) is re-validated, not read through the
+    stale pointer: a set_ onto new storage gives the new storage's result, a
+    resize_ / transpose_ to a bad layout raises."""
+    n = 128
+    rng = np.random.RandomState(6)
+    a, b = _env(gpu, n, 'post'), _env(gpu, n, 'post')
+    for e in (a, b):
+        e.reset(seed=4, options=dict(task_id=2))
+    qbuf = torch.tensor(rng.normal(size=(n, 15)), device=gpu)
+    vbuf = torch.tensor(rng.normal(size=(n, 14)), device=gpu)
+    a.wrap_step(qbuf, vbuf)  # cached
+    b.wrap_step(qbuf.clone(), vbuf.clone())
+    q2 = torch.tensor(rng.normal(size=(n, 15)), device=gpu)
+    qbuf.set_(q2.clone())  # same tensor object, new storage
+    got = [x.cpu().numpy().copy() for x in a.wrap_step(qbuf, vbuf)[:4]]
+    exp = [x.cpu().numpy().copy() for x in b.wrap_step(q2.clone(), vbuf.clone())[:4]]
+    for g_, e_ in zip(got, exp):
+        assert np.array_equal(g_, e_)
+    qbuf.resize_(n, 14)
+    with pytest.raises(ValueError):
+        a.wrap_step(qbuf, vbuf)
+    sq = torch.zeros(15, n, dtype=torch.float64, device=gpu)
+    z = torch.zeros(n, 15, dtype=torch.float64, device=gpu)
+    a.wrap_step(z, vbuf)
+    b.wrap_step(z.clone(), vbuf.clone())
+    sq.t_()  # (n, 15) but not contiguous: copied, same result as a contiguous copy
+    got = [x.cpu().numpy().copy() for x in a.wrap_step(sq, vbuf)[:4]]
+    exp = [x.cpu().numpy().copy() for x in b.wrap_step(sq.contiguous(), vbuf.clone())[:4]]
+    for g_, e_ in zip(got, exp):
+        assert np.array_equal(g_, e_)
+
+
+def test_reset_without_goal_states_warns_once(gpu):
+    env = _env(gpu, 8, 'post')
+    with pytest.warns(UserWarning, match='goal_states'):
+        env.reset(seed=1, options=dict(task_id=1))
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter('error')
+        env.reset(seed=1, options=dict(task_id=1))  # once per handle

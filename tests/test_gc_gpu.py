@@ -3,6 +3,7 @@
 injected draws, and against the oracle replaying the kernel's own Philox draws.
 All integer / gathered outputs are compared bit-exactly."""
 
+import functools
 import os
 
 import numpy as np
@@ -131,29 +132,77 @@ def test_plain_dataset_sample_and_random_idxs(gpu, gold):
     assert np.array_equal(sub['next_observations'].cpu().numpy(), data['observations'][nxt])
 
 
-def test_humanoid_scale_properties(gpu):
-    """BASELINE config shape (1M rows, obs 69, act 21, B=1024): size-independent
-    properties of a fused 64-batch launch."""
-    n_traj, L = 500, 2000
+@functools.lru_cache(maxsize=1)
+def humanoid_layout(n_traj=500, L=2000, seed=3):
+    """configs[3]'s buffer shape (1M rows, obs 69, act 21; equal trajectories,
+    the last row of each invalid) in the compact layout, as host arrays
+    (shared between tests: treat as read-only)."""
+    rng = np.random.default_rng(seed)
     R = n_traj * L
-    g = torch.Generator(device=gpu).manual_seed(3)
-    obs = torch.randn(R, 69, device=gpu, generator=g)
-    term = torch.zeros(R, device=gpu)
-    term[L - 1 :: L] = 1
-    valids = 1.0 - term
-    terms = torch.clamp(term + torch.cat([term[1:], torch.ones(1, device=gpu)]), max=1.0)
-    ds = Dataset(dict(observations=obs, actions=torch.randn(R, 21, device=gpu, generator=g), terminals=terms,
-                      valids=valids), device=gpu)
-    gc = GCDataset(ds, dict(CONFIGS['gciql'], discount=0.995, p_aug=None, frame_stack=None), seed=9)
+    term = np.zeros(R, np.float32)
+    term[L - 1::L] = 1
+    raw = dict(observations=rng.standard_normal((R, 69), dtype=np.float32),
+               actions=rng.standard_normal((R, 21), dtype=np.float32), terminals=term)
+    return orc.load_dataset(raw, compact_dataset=True)
+
+
+def test_humanoid_scale_properties(gpu):
+    """BASELINE configs[3] (1M rows, obs 69, act 21, B = 1024) through the
+    closed-form (periodic) path: a fused 64-batch Philox launch, every key --
+    rows, goal indices, masks, rewards -- bit-exact against the oracle fed the
+    draws the kernel reports, plus size-independent properties."""
+    L = 2000
+    data = humanoid_layout(L=L)
+    R = len(data['observations'])
+    ds = Dataset(data, device=gpu)
+    cfg = dict(CONFIGS['gciql'], discount=0.995, p_aug=None, frame_stack=None)
+    gc = GCDataset(ds, cfg, seed=9)
+    assert gc.period == (L, L - 1, L - 2)
     out = gc.sample(1024, num_batches=64, record_draws=True)
-    idx, vg, ag = out['_idxs'], out['_value_goal_idxs'], out['_actor_goal_idxs']
-    assert torch.equal(out['observations'], obs[idx])
-    assert torch.equal(out['next_observations'], obs[torch.clamp(idx + 1, max=R - 1)])
-    assert torch.equal(out['value_goals'], obs[vg])
-    assert torch.equal(out['actor_goals'], obs[ag])
-    assert torch.equal(out['actions'], ds['actions'][idx])
-    assert bool((valids[idx] == 1).all())
-    assert bool(((ag // L) == (idx // L)).all())
+    draws = {k: v.cpu().numpy() for k, v in out['_draws'].items()}
+    ref, idxs, vg, ag = orc.sample(data, cfg, draws)
+    assert np.array_equal(out['_idxs'].cpu().numpy(), idxs)
+    assert np.array_equal(out['_value_goal_idxs'].cpu().numpy(), vg)
+    assert np.array_equal(out['_actor_goal_idxs'].cpu().numpy(), ag)
+    assert set(ref) <= set(out)
+    for k, v in ref.items():
+        got = out[k].cpu().numpy()
+        assert got.dtype == v.dtype, k
+        assert np.array_equal(got, v), k
+    valids = data['valids']
+    assert (valids[idxs] == 1).all()
+    assert ((ag // L) == (idxs // L)).all()
+    assert abs(float((vg == idxs).mean()) - 0.2) < 0.01
+    assert R == 1_000_000
+
+
+def test_humanoid_scale_boundary_picks(gpu):
+    """The injected-draw kernel on the same 1M-row closed-form buffer, with the
+    sample / goal picks at every period boundary q*1999 - 1, q*1999 (and 0,
+    npick - 1), against the oracle."""
+    L = 2000
+    data = humanoid_layout(L=L)
+    ds = Dataset(data, device=gpu)
+    cfg = dict(CONFIGS['crl'], p_aug=None, frame_stack=None)
+    gc = GCDataset(ds, cfg, seed=2)
+    assert gc.period == (L, L - 1, L - 2)
+    npick = 500 * (L - 1)
+    q = np.arange(1, 500)
+    forced = np.concatenate([[0, npick - 1], q * (L - 1) - 1, q * (L - 1)])
+    rec = gc.sample(1024, record_draws=True)['_draws']
+    draws = {k: v.cpu().numpy() for k, v in rec.items()}
+    n = len(forced)
+    draws['pick'][:n] = forced
+    draws['v_pick'][:n] = forced[::-1]
+    draws['a_pick'][:n] = np.roll(forced, 7)
+    draws['v_geom'][:n] = np.arange(n) % 5 + 1  # goals at and just past the trajectory end
+    out = gc.sample(1024, draws=draws, record_draws=True)
+    ref, idxs, vg, ag = orc.sample(data, cfg, draws)
+    assert np.array_equal(out['_idxs'].cpu().numpy(), idxs)
+    assert np.array_equal(out['_value_goal_idxs'].cpu().numpy(), vg)
+    assert np.array_equal(out['_actor_goal_idxs'].cpu().numpy(), ag)
+    for k, v in ref.items():
+        assert np.array_equal(out[k].cpu().numpy(), v), k
 
 
 def test_out_reuse_matches_fresh_calls(gpu, gold):
@@ -204,3 +253,37 @@ def test_periodic_closed_form_matches_tables(gpu):
             x, y = a.sample(B, num_batches=nb), b.sample(B, num_batches=nb)
             for k in x:
                 assert torch.equal(x[k], y[k]), (cls.__name__, B, k)
+
+
+def test_row_record_stride_and_in_place_updates(gpu, gold):
+    """The sampler's packed copy of the small columns: its row
+    stride is the power of two at or above the packed bytes, it is skipped for
+    the plain sampler and under row_record=False, and a column modified in
+    place (or replaced) after the sampler was built is re-packed before the
+    next sample -- batches always show the dataset's current values."""
+    data = orc.load_dataset(_raw(gold), compact_dataset=True)  # actions 3 f32 + terminals + valids = 20 B
+    ds = Dataset(data, device=gpu)
+    cfg = dict(CONFIGS['gciql'], p_aug=None, frame_stack=None)
+    gc = GCDataset(ds, cfg, seed=3)
+    assert gc._rec_stride == 32 and gc._record.shape == (ds.size, 32)
+    assert ds._sampler()._record is None
+    off = GCDataset(ds, dict(cfg, row_record=False), seed=3)
+    assert off._record is None
+    a = gc.sample(512, record_draws=True)
+    b = off.sample(512, record_draws=True)
+    for k in a:
+        if not k.startswith('_'):
+            assert torch.equal(a[k], b[k]), k
+    prev = gc.sample(512)
+    ds['actions'].mul_(-2.0)  # in place: version counter moves
+    out = gc.sample(512, record_draws=True)
+    assert torch.equal(out['actions'], ds['actions'][out['_idxs']])
+    ds['terminals'].add_(0.0)
+    ds['actions'].add_(1.0)
+    refill = gc.sample(512, out=prev)
+    assert refill is prev
+    rows = ds['actions']
+    hit = (refill['actions'][:, None, :] == rows[None, :, :]).all(-1).any(-1)
+    assert bool(hit.all())  # every refilled row is a current dataset row
+    chk = gc.sample(512, record_draws=True)
+    assert torch.equal(chk['actions'], ds['actions'][chk['_idxs']])
