@@ -448,7 +448,7 @@ __device__ __forceinline__ void contact_loop(const PointModel& pm, const uint16_
 // end), so its collision runs beside this stage's solve.
 //
 // A lane bails to the full loop when its centre leaves the inner part of its
-// cell (e = h - X <= 0) or crosses to the far side of its step-start half
+// cell (e = h - X < 0) or crosses to the far side of its step-start half
 // (e >= h + 1.25, never reachable in a step: contacts move the centre by a
 // fraction of their penetration), or when its active set does not settle in
 // kLeanIters iterations.
@@ -458,7 +458,6 @@ struct LeanSides {
   // (the distance is then far positive: no contact, no compare against the
   // wall bit); rD likewise and the corner's squared-distance bound
   double rX, rY, rD, farD2;
-  uint32_t bX, bY, bD;  // the slot's edge bits on a wall side
 };
 
 __device__ __forceinline__ LeanSides lean_sides(const PointModel& pm, const RoleFrame& fr, double x, double y) {
@@ -474,9 +473,6 @@ __device__ __forceinline__ LeanSides lean_sides(const PointModel& pm, const Role
   L.rY = vY ? pm.radius : -1e3;
   L.rD = vD ? pm.radius : -1e3;
   L.farD2 = vD ? kPointFarD2 : -1.0;
-  L.bX = vX ? kSlotBits : 0u;
-  L.bY = vY ? kSlotBits << 3 : 0u;
-  L.bD = vD ? kSlotBits << 6 : 0u;
   return L;
 }
 
@@ -486,49 +482,82 @@ struct LeanHit {
   bool cX, cY, cD;
 };
 
-// Impedance gains of one slot without a branch or a band test: with
+// Impedance of one slot without a branch or a band test: with
 // x = min(|d| / width, 1), the power-2 sigmoid of solimp (mid 0.5) is
-// y = 2 x^2 - max(0, 2 x - 1)^2, imp = dmin + (dmax - dmin) y, and with
-// u = 1 - imp the gains are D = imp / (u diag) = (1/u - 1) / diag and
-// kp = K imp d.  Outside the band (x = 1) they are w_max and kp_max d to an
-// ulp.  The per-wave tail of a step is waves with a contact resting inside
-// the band (|d| < 1 mm) at every stage, so the band computation is part of
-// every stage rather than a branch those waves take 20 times.
+// y = 2 x^2 - max(0, 2 x - 1)^2 and imp = dmin + (dmax - dmin) y.  The gains
+// are D = imp / ((1 - imp) diag) and kp = K imp d; outside the band (x = 1)
+// they are w_max and kp_max d to an ulp.  The per-wave tail of a step is waves
+// with a contact resting inside the band (|d| < 1 mm) at every stage, so the
+// band computation is part of every stage rather than a branch those waves
+// take 20 times.  band_u returns u' = (1 - imp) / (dmax - dmin) = 2 - y
+// ((1 - dmin) / (dmax - dmin) = 2 to an ulp), so that every constant of the
+// formula is an inline operand; both clamps are the VOP3 clamp bit of the
+// producing v_mul / v_fma (x >= 0 and 2x - 1 <= 1, so clamping to [0, 1] is
+// exactly the min / max).
 static_assert(kPointModel.imp_mid == 0.5 && kPointModel.imp_a == 2.0 && kPointModel.imp_b == 2.0,
               "band_u assumes the default solimp midpoint and power");
+static_assert(kPointModel.imp_dmin == 0.9 && kPointModel.imp_dmax == 0.95,
+              "band_u assumes (1 - dmin) / (dmax - dmin) = 2");
+constexpr double kImpDelta = kPointModel.imp_dmax - kPointModel.imp_dmin;
+
 __device__ __forceinline__ double band_u(const PointModel& pm, double d) {
-  const double x = fmin(fabs(d) * pm.inv_width, 1.0);
-  const double m = fmax(fma(2.0, x, -1.0), 0.0);
-  const double y = fma(2.0 * x, x, -(m * m));
-  return fma(-(pm.imp_dmax - pm.imp_dmin), y, 1.0 - pm.imp_dmin);
+  const double x = fmin(fmax(fabs(d) * pm.inv_width, 0.0), 1.0);
+  const double m = fmin(fmax(fma(2.0, x, -1.0), 0.0), 1.0);
+  return fma(m, m, fma(-(x + x), x, 2.0));
 }
 
 #ifdef OGBX_WAVE_STAMPS
 __device__ unsigned long long g_wave_paths[4096];
 #endif
 
+// The slots of one stage, with the stage's normal equations SCALED: with
+// u'_s = (1 - imp_s) / (dmax - dmin) of slot s (band_u) and
+// P = diag (dmax - dmin) u'_0 u'_1 u'_2, the weight of slot s becomes
+// W_s = P w_s = imp_s prod_{t != s} u'_t -- products only, no reciprocal --
+// and the mass term mp = M P.  The unknown and the velocities of the lean
+// loop are carried divided by K (kp' = kp / K = imp d, mbp = m B P for the
+// scaled velocity): the edge tests compare kp with u, so they are
+// scale-invariant, and the position update uses h K.  The solution of the
+// scaled system is the solution.
+// A slot without a contact (no wall on that side, or a wall not touched) has
+// kp ~ 1e30: its three edges are then never active, so with its piece weights
+// 0 it contributes exactly nothing -- no validity mask and no weight select
+// in the stage.  A contact that ends during the step leaves stale active bits
+// for one check, which then differs from the new mask: the lane iterates once
+// (cold path) and drops them.
 struct LocalSlots {
-  double kp0, kp1, kp2, w0, w1, w2, nx2, ny2;
+  double kp0, kp1, kp2, w0, w1, w2, nx2, ny2, mp, mbp;
 };
 
+__device__ __forceinline__ double kp_or_far(bool on, double kp) {
+  // one v_cndmask on the high word: any low word with high word 0x46293E59
+  // is a positive double of about 1e30
+  return __hiloint2double(on ? __double2hiint(kp) : 0x46293E59, __double2loint(kp));
+}
+
 // Normal-equation solve of the piece with weights p (local role layout).
-__device__ __forceinline__ void local_piece_min(const PointModel& pm, const LocalSlots& c, const PieceWeights& p,
-                                                double mbvx, double mbvy, double* ux, double* uy) {
+__device__ __forceinline__ void local_piece_min(const LocalSlots& c, const PieceWeights& p, double vx, double vy,
+                                                double* ux, double* uy) {
 #pragma clang fp contract(fast)
-  const double M = pm.M;
   const double w0 = c.w0, w1 = c.w1, w2 = c.w2;
-  double h00 = M + w0 * p.S0 + w1 * p.T1;
-  double h11 = M + w0 * p.T0 + w1 * p.S1;
+  double h00 = c.mp + w0 * p.S0 + w1 * p.T1;
+  double h11 = c.mp + w0 * p.T0 + w1 * p.S1;
   double h01 = w0 * p.D0 - w1 * p.D1;
   const double g0 = w0 * c.kp0, g1 = w1 * c.kp1;
-  double r0 = mbvx + g0 * p.S0 - g1 * p.D1;
-  double r1 = mbvy + g0 * p.D0 + g1 * p.S1;
+  double r0 = c.mbp * vx + g0 * p.S0 - g1 * p.D1;
+  double r1 = c.mbp * vy + g0 * p.D0 + g1 * p.S1;
   const double nx = c.nx2, ny = c.ny2;
   const double q = nx * nx, s = ny * ny, o = nx * ny;
   const double WS = w2 * p.S2, WT = w2 * p.T2, WD = w2 * p.D2;
-  h00 += WS * q + WT * s - 2.0 * (WD * o);
-  h11 += WS * s + WT * q + 2.0 * (WD * o);
-  h01 += (WS - WT) * o + WD * (q - s);
+  const double t = WD * o;
+  h00 = fma(WS, q, h00);  // (chained: one fma per term, no partial sums)
+  h00 = fma(WT, s, h00);
+  h00 = fma(-2.0, t, h00);
+  h11 = fma(WS, s, h11);
+  h11 = fma(WT, q, h11);
+  h11 = fma(2.0, t, h11);
+  h01 = fma(WS - WT, o, h01);
+  h01 = fma(WD, q - s, h01);
   const double k2 = c.kp2;
   r0 -= k2 * (WS * nx - WD * ny);
   r1 -= k2 * (WS * ny + WD * nx);
@@ -549,46 +578,55 @@ __device__ __forceinline__ uint32_t local_edge_mask(const LocalSlots& c, double 
   return m;
 }
 
-__device__ __forceinline__ uint32_t local_slots(const PointModel& pm, const LeanSides& L, const LeanHit& k,
-                                                LocalSlots& c) {
+// M diag (dmax - dmin) and m B diag (dmax - dmin): mp and mbp per u'_0 u'_1 u'_2.
+constexpr double kMScale = kPointModel.M * kPointModel.diag * kImpDelta;
+constexpr double kMBScale = kPointModel.mass * kPointModel.B * kPointModel.diag * kImpDelta;
+// h K: the position increment per unit of scaled velocity.
+constexpr double kHK = kPointModel.h * kPointModel.K;
+
+__device__ __forceinline__ void local_slots(const PointModel& pm, const LeanHit& k, LocalSlots& c) {
   c.nx2 = -(k.ex * k.inv);
   c.ny2 = -(k.ey * k.inv);
   const double u0 = band_u(pm, k.d0), u1 = band_u(pm, k.d1), u2 = band_u(pm, k.d2);
-  const double p01 = u0 * u1, p = p01 * u2;
-  // u in [0.05, 0.1]: 1/(u0 u1 u2) by v_rcp_f64 and one Newton-Raphson step
-  // (2e-15 relative, fast_recip; the contact tolerance is 1e-9)
-  const double r = fast_recip(p);
-  const double r01 = r * u2;
-  const double idg = 1.0 / pm.diag;
-  c.w0 = k.cX ? fma(r01 * u1, idg, -idg) : 0.0;
-  c.w1 = k.cY ? fma(r01 * u0, idg, -idg) : 0.0;
-  c.w2 = k.cD ? fma(r * p01, idg, -idg) : 0.0;
-  c.kp0 = fma(-u0, pm.K, pm.K) * k.d0;
-  c.kp1 = fma(-u1, pm.K, pm.K) * k.d1;
-  c.kp2 = fma(-u2, pm.K, pm.K) * k.d2;
-  return (k.cX ? L.bX : 0u) | (k.cY ? L.bY : 0u) | (k.cD ? L.bD : 0u);
+  const double i0 = fma(-kImpDelta, u0, 1.0), i1 = fma(-kImpDelta, u1, 1.0), i2 = fma(-kImpDelta, u2, 1.0);
+  const double u01 = u0 * u1, u02 = u0 * u2, u12 = u1 * u2;
+  c.w0 = i0 * u12;
+  c.w1 = i1 * u02;
+  c.w2 = i2 * u01;
+  const double U = u01 * u2;
+  c.mp = kMScale * U;
+  c.mbp = kMBScale * U;
+  c.kp0 = kp_or_far(k.cX, i0 * k.d0);
+  c.kp1 = kp_or_far(k.cY, i1 * k.d1);
+  c.kp2 = kp_or_far(k.cD, i2 * k.d2);
 }
 
-// Slot distances at the local position (X, Y).  emin/emax track the smallest
-// and largest face offset e = h - X over the step (the bail test at the end).
-__device__ __forceinline__ void local_collide(const PointModel& pm, const LeanSides& L, double X, double Y,
-                                              LeanHit& k, double& emin, double& emax) {
-  const double hx = pm.box_hxy;
-  k.ex = hx - X;
-  k.ey = hx - Y;
-  emin = fmin(emin, fmin(k.ex, k.ey));
-  emax = fmax(emax, fmax(k.ex, k.ey));
-  k.d0 = k.ex - L.rX;
-  k.d1 = k.ey - L.rY;
-  const double d2 = fma(k.ex, k.ex, k.ey * k.ey);
+// Slot distances at the local face offsets (ex, ey) = (h - X, h - Y).  ehi
+// tracks the largest high word (as unsigned) of the offsets over the step: it
+// stays below that of h + 1.25 = 3.25 exactly while every e is in [+0, 3.25)
+// (a negative e sets the sign bit) -- the lean frame's validity, one
+// v_max3_u32 per stage.
+constexpr uint32_t kLeanEhiLimit = 0x400A0000u;  // high word of 3.25
+static_assert(kPointModel.box_hxy + 1.25 == 3.25, "kLeanEhiLimit is the high word of h + 1.25");
+
+__device__ __forceinline__ void local_collide(const LeanSides& L, double ex, double ey, LeanHit& k, uint32_t& ehi) {
+  k.ex = ex;
+  k.ey = ey;
+  // (asm: otherwise LLVM defers the max to the end of the step and keeps
+  // every stage's e alive in registers)
+  asm("v_max3_u32 %0, %1, %2, %3" : "=v"(ehi) : "v"(ehi), "v"(__double2hiint(ex)), "v"(__double2hiint(ey)));
+  k.d0 = ex - L.rX;
+  k.d1 = ey - L.rY;
+  const double d2 = fma(ex, ex, ey * ey);
   k.cX = k.d0 <= 0.0;
   k.cY = k.d1 <= 0.0;
   k.cD = !(d2 > L.farD2);
-  // e > 0 on both axes at every kept stage, so d2 > 0 (a lane with e <= 0
-  // bails and its values here are discarded)
+  // e >= 0 on both axes at every kept stage, so d2 >= 0 (a lane with e < 0
+  // bails and its values here are discarded; d2 = 0 only at the corner point
+  // itself, unreachable with a wall there)
   const double y0 = __builtin_amdgcn_rsq(d2);
   k.inv = y0 * fma(-0.5 * d2 * y0, y0, 1.5);
-  k.d2 = d2 * k.inv - L.rD;
+  k.d2 = fma(d2, k.inv, -L.rD);
 }
 
 // The lean loop of one step from (x, y) in frame fr; *bail on the lanes whose
@@ -601,67 +639,70 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
 #endif
   const double h = pm.h;
   const LeanSides L = lean_sides(pm, fr, x, y);
-  double emin = pm.box_hxy, emax = pm.box_hxy;
+  uint32_t ehi = 0;
   // local state: position, substep velocity, stage velocity, RK sums
-  double X = L.sxd * (x - L.cx), Y = L.syd * (y - L.cy);
+  // the face offsets E = h - X of the substep's start position (the loop
+  // carries E, not X: a stage's offsets are then one fma from its velocity)
+  double Ex = pm.box_hxy - L.sxd * (x - L.cx), Ey = pm.box_hxy - L.syd * (y - L.cy);
   double vx = 0.0, vy = 0.0, vsx = 0.0, vsy = 0.0;
   double sqx = 0.0, sqy = 0.0, svx = 0.0, svy = 0.0;
   LocalSlots c;
-  uint32_t valid;
   {
     LeanHit k0;
-    local_collide(pm, L, X, Y, k0, emin, emax);
-    valid = local_slots(pm, L, k0, c);
+    local_collide(L, Ex, Ey, k0, ehi);
+    local_slots(pm, k0, c);
   }
-  uint32_t act = local_edge_mask(c, 0.0, 0.0) & valid;
+  // first stage: v = 0, so the mask at u = cu = 0 (every edge of a penetrating
+  // contact) starts the iteration one step ahead of the empty set
+  uint32_t act = local_edge_mask(c, 0.0, 0.0);
   PieceWeights pw;
   piece_weights(act, pw);
-  const double mB = pm.mass * pm.B;
   const int nstage = 4 * pm.nsub;
 #pragma unroll 20
   for (int e = 0; e < nstage; ++e) {
     const int st = e & 3;
     const bool more = e + 1 < nstage;
-    double nqx, nqy, nsqx, nsqy, nx_ = X, ny_ = Y;
+    // the next stage's face offsets (velocities are carried divided by K, so
+    // the position increment is (h K) cf vs; cf = 1/2 folds into the
+    // constant exactly)
+    double nex, ney, nsqx, nsqy, nEx = Ex, nEy = Ey;
     {
 #pragma clang fp contract(fast)
       const double b = (st == 0 || st == 3) ? (1.0 / 6.0) : (1.0 / 3.0);
       nsqx = sqx + b * vsx;
       nsqy = sqy + b * vsy;
       if (st < 3) {
-        const double cf = (st < 2) ? 0.5 : 1.0;
-        nqx = X + h * (cf * vsx);
-        nqy = Y + h * (cf * vsy);
+        const double hcf = (st < 2) ? 0.5 * kHK : kHK;
+        nex = fma(-hcf, vsx, Ex);
+        ney = fma(-hcf, vsy, Ey);
       } else {
-        nx_ = X + h * nsqx;
-        ny_ = Y + h * nsqy;
-        nqx = nx_;
-        nqy = ny_;
+        nEx = fma(-kHK, nsqx, Ex);
+        nEy = fma(-kHK, nsqy, Ey);
+        nex = nEx;
+        ney = nEy;
       }
     }
     LeanHit k;
-    if (more) local_collide(pm, L, nqx, nqy, k, emin, emax);
+    if (more) local_collide(L, nex, ney, k, ehi);
     double ux, uy;
-    const double mbvx = mB * vsx, mbvy = mB * vsy;
-    local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+    local_piece_min(c, pw, vsx, vsy, &ux, &uy);
     uint32_t A2 = local_edge_mask(c, ux, uy);
     if (e == 0) {
       // The first stage's warm start (every penetrating edge active) is exact
       // for a single contact but wrong for about half of the multi-contact
       // lanes (53 % of all active-set iterations of a step were this stage's):
       // one semismooth Newton step for every lane here, in line.
-      act = A2 & valid;
+      act = A2;
       piece_weights(act, pw);
-      local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+      local_piece_min(c, pw, vsx, vsy, &ux, &uy);
       A2 = local_edge_mask(c, ux, uy);
     }
-    bool done = ((A2 ^ act) & valid) == 0u;
+    bool done = A2 == act;
     LocalSlots cn;
-    uint32_t valid_n = 0u;
-    if (more) valid_n = local_slots(pm, L, k, cn);
+    if (more) local_slots(pm, k, cn);
 #ifdef OGBX_PHYS_STATS
     if (!done) {
-      const int pc = __builtin_popcount((A2 ^ act) & valid);
+      const int pc = __builtin_popcount(A2 ^ act);
       OGBX_STAT(0);
       OGBX_STAT(pc == 1 ? 1 : (pc == 2 ? 2 : 3));
     }
@@ -676,11 +717,11 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
         OGBX_STAT(4);
         ++trips;
 #endif
-        act = A2 & valid;
+        act = A2;
         piece_weights(act, pw);
-        local_piece_min(pm, c, pw, mbvx, mbvy, &ux, &uy);
+        local_piece_min(c, pw, vsx, vsy, &ux, &uy);
         A2 = local_edge_mask(c, ux, uy);
-        done = ((A2 ^ act) & valid) == 0u;
+        done = A2 == act;
       }
       bl |= !done;
 #ifdef OGBX_PHYS_STATS
@@ -696,29 +737,26 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
       svx = svx + b * fx;
       svy = svy + b * fy;
       if (st < 3) {
-        const double cf = (st < 2) ? 0.5 : 1.0;
+        const double hcf = (st < 2) ? 0.5 * h : h;
         sqx = nsqx;
         sqy = nsqy;
-        vsx = vx + (cf * fx) * h;
-        vsy = vy + (cf * fy) * h;
+        vsx = fma(fx, hcf, vx);
+        vsy = fma(fy, hcf, vy);
       } else {
         vx = vx + svx * h;
         vy = vy + svy * h;
-        X = nx_;
-        Y = ny_;
+        Ex = nEx;
+        Ey = nEy;
         vsx = vx;
         vsy = vy;
         sqx = sqy = svx = svy = 0.0;
       }
     }
-    if (more) {
-      c = cn;
-      valid = valid_n;
-    }
+    if (more) c = cn;
   }
-  *bail = bl | !(emin > 0.0) | !(emax < pm.box_hxy + 1.25);
-  x = fma(L.sxd, X, L.cx);
-  y = fma(L.syd, Y, L.cy);
+  *bail = bl | !(ehi < kLeanEhiLimit);
+  x = fma(L.sxd, pm.box_hxy - Ex, L.cx);
+  y = fma(L.syd, pm.box_hxy - Ey, L.cy);
 #ifdef OGBX_WAVE_STAMPS
   {
     const unsigned long long b = __ballot(1);
