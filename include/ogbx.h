@@ -385,6 +385,26 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
                            int64_t* actor_goal_out, double* masks, double* rewards,
                            const ogbx_gc_draw_record* record, void* stream);
 
+/* Look-ahead sampling for a steady stream of equal calls (same batch,
+ * num_batches <= 1024 samples in total, Philox draws): the launch of call c
+ * gathers its rows from the selectors the launch of call c-1 stored in
+ * ahead_in (NULL: computed in this launch first) and, while it gathers,
+ * computes call c+1's selectors (Philox counter call_index + 1) into
+ * ahead_out (NULL: not computed), so a call's draw chain (Philox -> picks ->
+ * goals) is off its own critical path.  ahead_in / ahead_out are caller-owned
+ * device buffers of OGBX_GC_AHEAD_WORDS 8-byte words per sample, ordered on
+ * `stream`; ahead_in must hold what the previous launch stored for exactly
+ * this (seed, call_index, batch, num_batches, buffer, config).  Every output
+ * is bit-identical to ogbx_gc_sample's with the same seed and call_index.
+ * Same reference as ogbx_gc_sample (datasets.py:213-327). */
+#define OGBX_GC_AHEAD_WORDS 8
+ogbx_status ogbx_gc_sample_ahead(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                                 const ogbx_gc_column* cols, int32_t num_cols, int64_t batch,
+                                 int64_t num_batches, uint64_t seed, uint64_t call_index,
+                                 const int64_t* ahead_in, int64_t* ahead_out, int64_t* idxs_out,
+                                 int64_t* value_goal_out, int64_t* actor_goal_out, double* masks,
+                                 double* rewards, void* stream);
+
 /* ---- HGCDataset (impls/utils/datasets.py:467-643) ------------------------
  * Static config of the hierarchical sampler.  Subgoal steps are the resolved
  * values of the reference's config (value/actor default to
@@ -452,6 +472,17 @@ ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg
                             const ogbx_hgc_draws* draws, uint64_t seed, uint64_t call_index,
                             const ogbx_hgc_outputs* out, const ogbx_hgc_draw_record* record,
                             void* stream);
+
+/* HGCDataset.sample with look-ahead: ogbx_gc_sample_ahead's scheme for
+ * ogbx_hgc_sample (records of OGBX_HGC_AHEAD_WORDS words per sample: the ten
+ * row selectors and the nine scalar outputs).  Bit-identical to
+ * ogbx_hgc_sample with the same seed and call_index. */
+#define OGBX_HGC_AHEAD_WORDS 20
+ogbx_status ogbx_hgc_sample_ahead(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                                  const ogbx_hgc_config* hcfg, const ogbx_gc_column* cols, int32_t num_cols,
+                                  int64_t batch, int64_t num_batches, uint64_t seed, uint64_t call_index,
+                                  const int64_t* ahead_in, int64_t* ahead_out, const ogbx_hgc_outputs* out,
+                                  void* stream);
 
 /* traj_end[r] = terminal_locs[searchsorted(terminal_locs, r, 'left')] for
  * r in [0, R): binary search per row over the sorted terminal_locs

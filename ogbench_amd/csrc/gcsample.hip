@@ -129,18 +129,19 @@ __device__ inline int64_t geometric_from(double u, double log_q) {
   return g < 1.0 ? 1 : (int64_t)g;
 }
 
+// Threads [t0, blockDim.x) copy (t0 = 64: the first wave is busy elsewhere).
 template <typename T>
 __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, int64_t base,
-                                 int tile) {
+                                 int tile, int t0) {
   const int64_t units = col.row_bytes / (int64_t)sizeof(T);
   const int64_t pitch = src_pitch<T>(col);
   const T* __restrict__ src = (const T*)col.src;
   T* __restrict__ dst = (T*)col.dst;
   const int64_t total = units * tile;
-  const int step = blockDim.x;
-  int64_t b = threadIdx.x / units, k = threadIdx.x % units;
+  const int step = blockDim.x - t0, tid = threadIdx.x - t0;
+  int64_t b = tid / units, k = tid % units;
   const int64_t sb = step / units, sk = step % units;
-  for (int64_t f = threadIdx.x; f < total; f += step) {
+  for (int64_t f = tid; f < total; f += step) {
     dst[(base + b) * units + k] = src[sel[b] * pitch + k];
     k += sk;
     b += sb;
@@ -158,13 +159,16 @@ __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, 
 // cover the row's words, and each wave issues the loads of up to kJ jobs
 // before any store, so all column rows of the tile share one HBM round trip.
 // Otherwise each column is copied with its widest aligned unit.
+// Waves [wave0, blockDim.x / 64) copy (wave0 = 1: the first wave computes the
+// next call's selectors meanwhile, gc_ahead_kernel).
 template <int kSel>
 __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int64_t (*sel)[kGcMaxTile], int64_t base,
-                                 int n_here, bool flat4) {
+                                 int n_here, bool flat4, int wave0 = 0) {
+  if ((int)(threadIdx.x >> 6) < wave0) return;
   if (flat4) {
     constexpr int kJ = 8, kSlots = 2;
-    const int nw = (int)(blockDim.x >> 6);
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nw = (int)(blockDim.x >> 6) - wave0;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - wave0;
     const int lane = (int)(threadIdx.x & 63);
     const int jobs = num_cols * n_here;
     for (int j0 = wave; j0 < jobs; j0 += nw * kJ) {
@@ -203,14 +207,15 @@ __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int6
     const ogbx_gc_column& col = cols.c[c];
     const int64_t* srow = sel[col.select];
     const uintptr_t align = (uintptr_t)col.src | (uintptr_t)col.dst | (uintptr_t)col.src_stride;
+    const int t0 = 64 * wave0;
     if (col.row_bytes % 16 == 0 && align % 16 == 0)
-      copy_rows<uint4>(col, srow, base, n_here);
+      copy_rows<uint4>(col, srow, base, n_here, t0);
     else if (col.row_bytes % 8 == 0 && align % 8 == 0)
-      copy_rows<uint2>(col, srow, base, n_here);
+      copy_rows<uint2>(col, srow, base, n_here, t0);
     else if (col.row_bytes % 4 == 0 && align % 4 == 0)
-      copy_rows<uint32_t>(col, srow, base, n_here);
+      copy_rows<uint32_t>(col, srow, base, n_here, t0);
     else
-      copy_rows<uint8_t>(col, srow, base, n_here);
+      copy_rows<uint8_t>(col, srow, base, n_here, t0);
   }
 }
 
@@ -338,6 +343,125 @@ __global__ void __launch_bounds__(256) gc_sample_kernel(
   }
   __syncthreads();
   copy_tile<0>(cols, num_cols, sel, base, n_here, flat4);
+}
+
+// ---------------------------------------------------------------- look-ahead
+// One sample's selectors and scalars, as GCDataset.sample draws them with the
+// Philox words w0..w4 (the same arithmetic as gc_sample_kernel's Philox path).
+struct GcPick {
+  int64_t idx, next, vg, ag;
+  double mask, reward;
+};
+
+__device__ inline GcPick gc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_config& cfg, const u32x4& w0,
+                                  const u32x4& w1, const u32x4& w2, const u32x4& w3, const u32x4& w4,
+                                  double v_log_q, double a_log_q) {
+  const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
+  const int64_t pick = (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
+  GoalDraws v, a;
+  v.pick = (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
+  a.pick = (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+  int64_t idx = 0, final_idx;
+  index_loads(buf, false, pick, &idx, &final_idx);
+  const int64_t v_rand = cfg.value_cur_is_one ? 0 : rand_goal_of(buf, v.pick);
+  const int64_t a_rand = cfg.actor_cur_is_one ? 0 : rand_goal_of(buf, a.pick);
+  const double uvg = u01_from(w1.z, w1.w), uag = u01_from(w2.x, w2.y);
+  v.geom = cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0;
+  a.geom = cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0;
+  v.dist = uvg;
+  a.dist = uag;
+  v.u_traj = u01_from(w2.z, w2.w);
+  v.u_cur = u01_from(w3.x, w3.y);
+  a.u_traj = u01_from(w3.z, w3.w);
+  a.u_cur = u01_from(w4.x, w4.y);
+  GcPick p;
+  p.idx = idx;
+  p.next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
+  p.vg = sample_goal(idx, final_idx, v, v_rand, cfg.value_p_curgoal, cfg.value_traj_thresh, cfg.value_geom_sample,
+                     cfg.value_cur_is_one);
+  p.ag = sample_goal(idx, final_idx, a, a_rand, cfg.actor_p_curgoal, cfg.actor_traj_thresh, cfg.actor_geom_sample,
+                     cfg.actor_cur_is_one);
+  const double succ = idx == p.vg ? 1.0 : 0.0;
+  p.mask = 1.0 - succ;
+  p.reward = succ - (cfg.gc_negative ? 1.0 : 0.0);
+  return p;
+}
+
+// The first wave's chain of sample s under call (lo, hi): lanes 0..4 each run
+// one Philox call, every lane then runs the chain on the broadcast words (a
+// chain on one active lane issues about twice as slowly).
+__device__ inline GcPick gc_wave_chain(const ogbx_gc_buffer& buf, const ogbx_gc_config& cfg, int64_t s, uint32_t lo,
+                                       uint32_t hi, uint32_t k0, uint32_t k1, double v_log_q, double a_log_q) {
+  const uint64_t su = (uint64_t)s;
+  const uint32_t q = (uint32_t)(threadIdx.x & 63) % 5u;
+  const u32x4 w = philox4x32_10({(uint32_t)su, lo, q, (uint32_t)(su >> 32) ^ hi}, k0, k1);
+  u32x4 ws[5];
+#pragma unroll
+  for (int c = 0; c < 5; ++c)
+    ws[c] = u32x4{(uint32_t)__builtin_amdgcn_readlane((int)w.x, c), (uint32_t)__builtin_amdgcn_readlane((int)w.y, c),
+                  (uint32_t)__builtin_amdgcn_readlane((int)w.z, c), (uint32_t)__builtin_amdgcn_readlane((int)w.w, c)};
+  return gc_chain(buf, cfg, ws[0], ws[1], ws[2], ws[3], ws[4], v_log_q, a_log_q);
+}
+
+// GCDataset.sample with look-ahead (one sample per workgroup, Philox draws):
+// the selectors of this call come from ahead_in (stored by the previous
+// call's launch; NULL: computed here first), and while waves 1..3 gather the
+// rows, the first wave computes the NEXT call's selectors (call next_lo/hi)
+// into ahead_out.  The draw chain of a call is thereby off its own critical
+// path.  Words per sample (kGcAheadWords): idx, next, value goal, actor goal,
+// mask, reward.
+constexpr int kGcAheadWords = OGBX_GC_AHEAD_WORDS;
+constexpr int64_t kGcAheadMaxSamples = 1024;
+
+__global__ void __launch_bounds__(256) gc_ahead_kernel(
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, GcColumns cols, int32_t num_cols, uint32_t k0, uint32_t k1,
+    uint32_t call_lo, uint32_t call_hi, uint32_t next_lo, uint32_t next_hi, double v_log_q, double a_log_q,
+    const int64_t* __restrict__ ahead_in, int64_t* __restrict__ ahead_out, int64_t* idxs_out, int64_t* vgoal_out,
+    int64_t* agoal_out, double* masks, double* rewards, bool flat4) {
+  __shared__ int64_t sel[4][kGcMaxTile];
+  const int64_t s = xcd_tile();
+  const int t = (int)threadIdx.x;
+  auto publish = [&](const GcPick& p) {
+    sel[0][0] = p.idx;
+    sel[1][0] = p.next;
+    sel[2][0] = p.vg;
+    sel[3][0] = p.ag;
+    if (idxs_out) idxs_out[s] = p.idx;
+    if (vgoal_out) vgoal_out[s] = p.vg;
+    if (agoal_out) agoal_out[s] = p.ag;
+    masks[s] = p.mask;
+    rewards[s] = p.reward;
+  };
+  if (ahead_in) {
+    if (t < 3) {
+      const longlong2 v = reinterpret_cast<const longlong2*>(ahead_in + s * kGcAheadWords)[t];
+      if (t < 2) {
+        sel[2 * t][0] = v.x;
+        sel[2 * t + 1][0] = v.y;
+        if (t == 0 && idxs_out) idxs_out[s] = v.x;
+        if (t == 1 && vgoal_out) vgoal_out[s] = v.x;
+        if (t == 1 && agoal_out) agoal_out[s] = v.y;
+      } else {
+        masks[s] = __longlong_as_double(v.x);
+        rewards[s] = __longlong_as_double(v.y);
+      }
+    }
+  } else if (t < 64) {
+    const GcPick p = gc_wave_chain(buf, cfg, s, call_lo, call_hi, k0, k1, v_log_q, a_log_q);
+    if (t == 0) publish(p);
+  }
+  __syncthreads();
+  if (ahead_out && t < 64) {
+    const GcPick p = gc_wave_chain(buf, cfg, s, next_lo, next_hi, k0, k1, v_log_q, a_log_q);
+    if (t == 0) {
+      longlong2* o = reinterpret_cast<longlong2*>(ahead_out + s * kGcAheadWords);
+      o[0] = make_longlong2(p.idx, p.next);
+      o[1] = make_longlong2(p.vg, p.ag);
+      o[2] = make_longlong2(__double_as_longlong(p.mask), __double_as_longlong(p.reward));
+    }
+  } else {
+    copy_tile<0>(cols, num_cols, sel, s, 1, flat4, ahead_out ? 1 : 0);
+  }
 }
 
 // HGCDataset.compute_high_next_idxs (datasets.py:478-491) for one sample.
@@ -496,6 +620,177 @@ __global__ void __launch_bounds__(256) hgc_sample_kernel(
   copy_tile<0>(cols, num_cols, sel, base, n_here, flat4);
 }
 
+// HGC look-ahead: one sample's ten selectors and nine scalar outputs (the
+// order of ogbx_hgc_outputs from high_value_offsets on), as hgc_sample_kernel's
+// Philox path computes them.
+struct HgcPick {
+  int64_t sel[kHgcSel];
+  int64_t w[9];  // offsets, hv steps, hv mask, hv reward, lv steps, lv mask, lv reward, mask, reward (f64 as bits)
+};
+
+__device__ inline HgcPick hgc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_config& cfg, const ogbx_hgc_config& hc,
+                                    const u32x4* wv, double v_log_q, double a_log_q, double l_log_q) {
+  const u32x4 w0 = wv[0], w1 = wv[1], w2 = wv[2], w3 = wv[3], w4 = wv[4];
+  const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
+  const int64_t pick = (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
+  GoalDraws v, a, l;
+  v.pick = (int64_t)bounded64(w0.z, w0.w, (uint64_t)npick);
+  a.pick = (int64_t)bounded64(w1.x, w1.y, (uint64_t)npick);
+  u32x4 w5{}, w6{};
+  int64_t l_rand = 0;
+  if (hc.has_low_value_goals) {
+    w5 = wv[5];
+    w6 = wv[6];
+    l.pick = (int64_t)bounded64(w5.x, w5.y, (uint64_t)npick);
+  }
+  int64_t idx = 0, fin;
+  index_loads(buf, false, pick, &idx, &fin);
+  const int64_t v_rand = cfg.value_cur_is_one ? 0 : rand_goal_of(buf, v.pick);
+  const int64_t a_rand = cfg.actor_cur_is_one ? 0 : rand_goal_of(buf, a.pick);
+  if (hc.has_low_value_goals && !cfg.value_cur_is_one) l_rand = rand_goal_of(buf, l.pick);
+  const int64_t next = idx + 1 < buf.num_rows ? idx + 1 : buf.num_rows - 1;
+  const double uvg = u01_from(w1.z, w1.w), uag = u01_from(w2.x, w2.y);
+  v.geom = cfg.value_geom_sample ? geometric_from(uvg, v_log_q) : 0;
+  a.geom = cfg.actor_geom_sample ? geometric_from(uag, a_log_q) : 0;
+  v.dist = uvg;
+  a.dist = uag;
+  v.u_traj = u01_from(w2.z, w2.w);
+  v.u_cur = u01_from(w3.x, w3.y);
+  a.u_traj = u01_from(w3.z, w3.w);
+  a.u_cur = u01_from(w4.x, w4.y);
+  const int64_t hvg = sample_goal(idx, fin, v, v_rand, cfg.value_p_curgoal, cfg.value_traj_thresh,
+                                  cfg.value_geom_sample, cfg.value_cur_is_one);
+  const int64_t hag = sample_goal(idx, fin, a, a_rand, cfg.actor_p_curgoal, cfg.actor_traj_thresh,
+                                  cfg.actor_geom_sample, cfg.actor_cur_is_one);
+  int64_t lvg = idx;
+  if (hc.has_low_value_goals) {
+    l.geom = geometric_from(u01_from(w5.z, w5.w), l_log_q);
+    l.dist = 0.0;
+    l.u_traj = u01_from(w6.x, w6.y);
+    l.u_cur = u01_from(w6.z, w6.w);
+    lvg = sample_goal(idx, fin, l, l_rand, cfg.value_p_curgoal, cfg.value_traj_thresh, 1, cfg.value_cur_is_one);
+  }
+  int64_t hv_next, hv_steps, lv_next, lv_steps, ha_next, ha_steps, la_next, la_steps;
+  high_next(idx, fin, hvg, hc.value_subgoal_steps, &hv_next, &hv_steps);
+  high_next(idx, fin, hvg, hc.low_subgoal_steps, &lv_next, &lv_steps);
+  high_next(idx, fin, hag, hc.actor_subgoal_steps, &ha_next, &ha_steps);
+  const int64_t la_goal = idx + hc.actor_subgoal_steps < fin ? idx + hc.actor_subgoal_steps : fin;
+  high_next(idx, fin, hag, hc.low_subgoal_steps, &la_next, &la_steps);
+  HgcPick p;
+  p.sel[0] = idx;
+  p.sel[1] = next;
+  p.sel[2] = hvg;
+  p.sel[3] = hag;
+  p.sel[4] = hv_next;
+  p.sel[5] = lv_next;
+  p.sel[6] = lvg;
+  p.sel[7] = ha_next;
+  p.sel[8] = la_goal;
+  p.sel[9] = la_next;
+  const double neg = cfg.gc_negative ? 1.0 : 0.0;
+  p.w[0] = hvg - idx;
+  p.w[1] = hv_steps;
+  p.w[2] = __double_as_longlong(hc.hv_mask_table[hv_steps]);
+  p.w[3] = __double_as_longlong(hc.hv_reward_table[hv_steps]);
+  p.w[4] = lv_steps;
+  if (hc.has_low_value_goals) {
+    const double ls = idx == lvg ? 1.0 : 0.0;
+    p.w[5] = __double_as_longlong(1.0 - ls);
+    p.w[6] = __double_as_longlong(ls - neg);
+  } else {
+    p.w[5] = __double_as_longlong(hc.lv_mask_table[lv_steps]);
+    p.w[6] = __double_as_longlong(hc.lv_reward_table[lv_steps]);
+  }
+  const double succ = idx == hvg ? 1.0 : 0.0;
+  p.w[7] = __double_as_longlong(1.0 - succ);
+  p.w[8] = __double_as_longlong(succ - neg);
+  return p;
+}
+
+__device__ inline HgcPick hgc_wave_chain(const ogbx_gc_buffer& buf, const ogbx_gc_config& cfg,
+                                         const ogbx_hgc_config& hc, int64_t s, uint32_t lo, uint32_t hi, uint32_t k0,
+                                         uint32_t k1, double v_log_q, double a_log_q, double l_log_q) {
+  const uint64_t su = (uint64_t)s;
+  const uint32_t calls = hc.has_low_value_goals ? 7u : 5u;
+  const uint32_t q = (uint32_t)(threadIdx.x & 63) % calls;
+  const u32x4 w = philox4x32_10({(uint32_t)su, lo, q, (uint32_t)(su >> 32) ^ hi}, k0, k1);
+  u32x4 ws[7];
+#pragma unroll
+  for (int c = 0; c < 7; ++c)
+    ws[c] = u32x4{(uint32_t)__builtin_amdgcn_readlane((int)w.x, c), (uint32_t)__builtin_amdgcn_readlane((int)w.y, c),
+                  (uint32_t)__builtin_amdgcn_readlane((int)w.z, c), (uint32_t)__builtin_amdgcn_readlane((int)w.w, c)};
+  return hgc_chain(buf, cfg, hc, ws, v_log_q, a_log_q, l_log_q);
+}
+
+constexpr int kHgcAheadWords = OGBX_HGC_AHEAD_WORDS;
+static_assert(kHgcAheadWords >= kHgcSel + 9, "HGC look-ahead record: 10 selectors + 9 scalars");
+
+// HGCDataset.sample with look-ahead (gc_ahead_kernel's scheme).
+__global__ void __launch_bounds__(256) hgc_ahead_kernel(
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, GcColumns cols, int32_t num_cols, uint32_t k0,
+    uint32_t k1, uint32_t call_lo, uint32_t call_hi, uint32_t next_lo, uint32_t next_hi, double v_log_q,
+    double a_log_q, double l_log_q, const int64_t* __restrict__ ahead_in, int64_t* __restrict__ ahead_out,
+    ogbx_hgc_outputs o, bool flat4) {
+  __shared__ int64_t sel[kHgcSel][kGcMaxTile];
+  const int64_t s = xcd_tile();
+  const int t = (int)threadIdx.x;
+  // scalar word j (0..8) of a record -> its output (static j: no pointer array)
+  auto put_scalar = [&](int j, int64_t v) {
+    switch (j) {
+      case 0: o.high_value_offsets[s] = v; break;
+      case 1: o.high_value_subgoal_steps[s] = v; break;
+      case 2: o.high_value_masks[s] = __longlong_as_double(v); break;
+      case 3: o.high_value_rewards[s] = __longlong_as_double(v); break;
+      case 4: o.low_value_subgoal_steps[s] = v; break;
+      case 5: o.low_value_masks[s] = __longlong_as_double(v); break;
+      case 6: o.low_value_rewards[s] = __longlong_as_double(v); break;
+      case 7: o.masks[s] = __longlong_as_double(v); break;
+      default: o.rewards[s] = __longlong_as_double(v); break;
+    }
+  };
+  auto put_index = [&](int k, int64_t v) {
+    if (k == 0 && o.idxs) o.idxs[s] = v;
+    if (k == 2 && o.high_value_goal_idxs) o.high_value_goal_idxs[s] = v;
+    if (k == 3 && o.high_actor_goal_idxs) o.high_actor_goal_idxs[s] = v;
+    if (k == 6 && o.low_value_goal_idxs) o.low_value_goal_idxs[s] = v;
+  };
+  if (ahead_in) {
+    if (t < kHgcSel + 9) {
+      const int64_t v = ahead_in[s * kHgcAheadWords + t];
+      if (t < kHgcSel) {
+        sel[t][0] = v;
+        put_index(t, v);
+      } else {
+        put_scalar(t - kHgcSel, v);
+      }
+    }
+  } else if (t < 64) {
+    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, call_lo, call_hi, k0, k1, v_log_q, a_log_q, l_log_q);
+    if (t == 0) {
+#pragma unroll
+      for (int k = 0; k < kHgcSel; ++k) {
+        sel[k][0] = p.sel[k];
+        put_index(k, p.sel[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < 9; ++j) put_scalar(j, p.w[j]);
+    }
+  }
+  __syncthreads();
+  if (ahead_out && t < 64) {
+    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, next_lo, next_hi, k0, k1, v_log_q, a_log_q, l_log_q);
+    if (t == 0) {
+      int64_t* r = ahead_out + s * kHgcAheadWords;
+#pragma unroll
+      for (int k = 0; k < kHgcSel; ++k) r[k] = p.sel[k];
+#pragma unroll
+      for (int j = 0; j < 9; ++j) r[kHgcSel + j] = p.w[j];
+    }
+  } else {
+    copy_tile<0>(cols, num_cols, sel, s, 1, flat4, ahead_out ? 1 : 0);
+  }
+}
+
 __global__ void traj_end_kernel(const int64_t* __restrict__ term, int64_t nterm, int64_t nrows,
                                 int64_t* __restrict__ out) {
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -599,6 +894,44 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
   return OGBX_OK;
 }
 
+ogbx_status ogbx_gc_sample_ahead(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                                 const ogbx_gc_column* cols, int32_t num_cols, int64_t batch,
+                                 int64_t num_batches, uint64_t seed, uint64_t call_index,
+                                 const int64_t* ahead_in, int64_t* ahead_out, int64_t* idxs_out,
+                                 int64_t* value_goal_out, int64_t* actor_goal_out, double* masks,
+                                 double* rewards, void* stream) {
+  OGBX_CHECK(buf && cfg && masks && rewards, OGBX_EINVAL, "ogbx_gc_sample_ahead: null argument");
+  OGBX_CHECK(num_cols >= 0 && num_cols <= kGcMaxCols, OGBX_EINVAL, "ogbx_gc_sample_ahead: at most 32 columns");
+  OGBX_CHECK(batch > 0 && num_batches > 0, OGBX_EINVAL, "batch and num_batches must be > 0");
+  const int64_t total = batch * num_batches;
+  OGBX_CHECK(total <= kGcAheadMaxSamples, OGBX_EINVAL,
+             "ogbx_gc_sample_ahead: at most 1024 samples per call (one per workgroup)");
+  OGBX_CHECK(buf->num_rows > 0 && buf->traj_end, OGBX_EINVAL, "empty trajectory buffer");
+  OGBX_CHECK(buf->valid_idxs == nullptr || buf->num_valid > 0, OGBX_EINVAL, "no valid transitions in the dataset");
+  OGBX_CHECK(periodic_ok(*buf), OGBX_EINVAL, "ogbx_gc_buffer: inconsistent period fields");
+  OGBX_CHECK(ahead_in != ahead_out || ahead_in == nullptr, OGBX_EINVAL,
+             "ogbx_gc_sample_ahead: ahead_in and ahead_out must differ");
+  GcColumns cc{};
+  for (int i = 0; i < num_cols; ++i) {
+    OGBX_CHECK(cols[i].src_stride == 0 || cols[i].src_stride >= cols[i].row_bytes, OGBX_EINVAL,
+               "ogbx_gc_sample_ahead: src_stride below row_bytes");
+    OGBX_CHECK(cols[i].src && cols[i].dst && cols[i].row_bytes > 0 && cols[i].select >= 0 && cols[i].select <= 3,
+               OGBX_EINVAL, "ogbx_gc_sample_ahead: bad column descriptor");
+    cc.c[i] = cols[i];
+  }
+  uint32_t k0, k1;
+  seed_key(seed, kTagGcSample, &k0, &k1);
+  const double v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
+  const double a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
+  const uint64_t next = call_index + 1;
+  hipLaunchKernelGGL(gc_ahead_kernel, dim3((uint32_t)total), dim3(256), 0, (hipStream_t)stream, *buf, *cfg, cc,
+                     num_cols, k0, k1, (uint32_t)call_index, (uint32_t)(call_index >> 32), (uint32_t)next,
+                     (uint32_t)(next >> 32), v_log_q, a_log_q, ahead_in, ahead_out, idxs_out, value_goal_out,
+                     actor_goal_out, masks, rewards, flat4_columns(cc, num_cols));
+  OGBX_LAUNCHED("gc_ahead_kernel");
+  return OGBX_OK;
+}
+
 ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
                             const ogbx_hgc_config* hcfg, const ogbx_gc_column* cols,
                             int32_t num_cols, int64_t batch, int64_t num_batches,
@@ -652,6 +985,55 @@ ogbx_status ogbx_hgc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg
                      (uint32_t)(call_index >> 32), v_log_q, a_log_q, l_log_q, *out, rec,
                      tile <= 4 && flat4_columns(cc, num_cols));
   OGBX_LAUNCHED("hgc_sample_kernel");
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_hgc_sample_ahead(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                                  const ogbx_hgc_config* hcfg, const ogbx_gc_column* cols, int32_t num_cols,
+                                  int64_t batch, int64_t num_batches, uint64_t seed, uint64_t call_index,
+                                  const int64_t* ahead_in, int64_t* ahead_out, const ogbx_hgc_outputs* out,
+                                  void* stream) {
+  OGBX_CHECK(buf && cfg && hcfg && out, OGBX_EINVAL, "ogbx_hgc_sample_ahead: null argument");
+  OGBX_CHECK(out->high_value_offsets && out->high_value_subgoal_steps && out->high_value_masks &&
+                 out->high_value_rewards && out->low_value_subgoal_steps && out->low_value_masks &&
+                 out->low_value_rewards && out->masks && out->rewards,
+             OGBX_EINVAL, "ogbx_hgc_sample_ahead: missing scalar output");
+  OGBX_CHECK(hcfg->hv_mask_table && hcfg->hv_reward_table && hcfg->lv_mask_table && hcfg->lv_reward_table,
+             OGBX_EINVAL, "ogbx_hgc_sample_ahead: missing reward/mask tables");
+  OGBX_CHECK(hcfg->value_subgoal_steps >= 0 && hcfg->low_subgoal_steps >= 0 && hcfg->actor_subgoal_steps >= 0,
+             OGBX_EINVAL, "ogbx_hgc_sample_ahead: negative subgoal steps");
+  OGBX_CHECK(!hcfg->has_low_value_goals || (hcfg->low_discount > 0.0 && hcfg->low_discount < 1.0), OGBX_EINVAL,
+             "ogbx_hgc_sample_ahead: low_discount must be in (0, 1)");
+  OGBX_CHECK(num_cols >= 0 && num_cols <= kGcMaxCols, OGBX_EINVAL, "ogbx_hgc_sample_ahead: at most 32 columns");
+  OGBX_CHECK(batch > 0 && num_batches > 0, OGBX_EINVAL, "batch and num_batches must be > 0");
+  const int64_t total = batch * num_batches;
+  OGBX_CHECK(total <= kGcAheadMaxSamples, OGBX_EINVAL,
+             "ogbx_hgc_sample_ahead: at most 1024 samples per call (one per workgroup)");
+  OGBX_CHECK(buf->num_rows > 0 && buf->traj_end, OGBX_EINVAL, "empty trajectory buffer");
+  OGBX_CHECK(buf->valid_idxs == nullptr || buf->num_valid > 0, OGBX_EINVAL, "no valid transitions in the dataset");
+  OGBX_CHECK(periodic_ok(*buf), OGBX_EINVAL, "ogbx_gc_buffer: inconsistent period fields");
+  OGBX_CHECK(ahead_in != ahead_out || ahead_in == nullptr, OGBX_EINVAL,
+             "ogbx_hgc_sample_ahead: ahead_in and ahead_out must differ");
+  GcColumns cc{};
+  for (int i = 0; i < num_cols; ++i) {
+    OGBX_CHECK(cols[i].src_stride == 0 || cols[i].src_stride >= cols[i].row_bytes, OGBX_EINVAL,
+               "ogbx_hgc_sample_ahead: src_stride below row_bytes");
+    OGBX_CHECK(cols[i].src && cols[i].dst && cols[i].row_bytes > 0 && cols[i].select >= 0 &&
+                   cols[i].select < kHgcSel,
+               OGBX_EINVAL, "ogbx_hgc_sample_ahead: bad column descriptor");
+    cc.c[i] = cols[i];
+  }
+  uint32_t k0, k1;
+  seed_key(seed, kTagHgcSample, &k0, &k1);
+  const double v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
+  const double a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
+  const double l_log_q = hcfg->has_low_value_goals ? std::log(1.0 - (1.0 - hcfg->low_discount)) : 0.0;
+  const uint64_t next = call_index + 1;
+  hipLaunchKernelGGL(hgc_ahead_kernel, dim3((uint32_t)total), dim3(256), 0, (hipStream_t)stream, *buf, *cfg, *hcfg,
+                     cc, num_cols, k0, k1, (uint32_t)call_index, (uint32_t)(call_index >> 32), (uint32_t)next,
+                     (uint32_t)(next >> 32), v_log_q, a_log_q, l_log_q, ahead_in, ahead_out, *out,
+                     flat4_columns(cc, num_cols));
+  OGBX_LAUNCHED("hgc_ahead_kernel");
   return OGBX_OK;
 }
 

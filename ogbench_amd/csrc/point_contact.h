@@ -578,6 +578,45 @@ __device__ __forceinline__ uint32_t local_edge_mask(const LocalSlots& c, double 
   return m;
 }
 
+// The active set as nine wave masks (bit l of m[e]: edge e of lane l is
+// active): the stage's consistency check then runs on the scalar unit -- each
+// edge test's v_cmp result IS a wave mask -- instead of packing nine
+// per-lane bits with v_cndmask / v_or3.
+struct EdgeWaves {
+  uint64_t m[9];
+};
+
+__device__ __forceinline__ void edge_waves(uint32_t act, EdgeWaves& w) {
+#pragma unroll
+  for (int e = 0; e < 9; ++e) w.m[e] = __ballot((act >> e) & 1u);
+}
+
+// acc | (m ^ a) on the scalar unit: two SALU ops (written out: LLVM turns the
+// OR of XORs into nine compare-and-select triples).
+__device__ __forceinline__ uint64_t or_xor(uint64_t acc, uint64_t m, uint64_t a) {
+  uint64_t x;
+  asm("s_xor_b64 %0, %1, %2\n\ts_or_b64 %0, %0, %3" : "=&s"(x) : "s"(m), "s"(a), "s"(acc) : "scc");
+  return x;
+}
+
+// Lanes whose edge mask at U differs from the active set w (local_edge_mask's
+// tests, bit for bit).
+__device__ __forceinline__ uint64_t edge_mismatch(const LocalSlots& c, double ux, double uy, const EdgeWaves& w) {
+#pragma clang fp contract(fast)
+  const double P = ux + uy, Q = ux - uy;
+  const double a = c.nx2 * ux + (c.ny2 * uy + c.kp2);
+  const double b = c.nx2 * uy - c.ny2 * ux;
+  uint64_t mis = __ballot(c.kp0 < P) ^ w.m[0];
+  mis = or_xor(mis, __ballot(c.kp0 < Q), w.m[1]);
+  mis = or_xor(mis, __ballot(c.kp0 < ux), w.m[2]);
+  mis = or_xor(mis, __ballot(c.kp1 < -Q), w.m[3]);
+  mis = or_xor(mis, __ballot(c.kp1 < P), w.m[4]);
+  mis = or_xor(mis, __ballot(c.kp1 < uy), w.m[5]);
+  mis = or_xor(mis, __ballot(a < -b), w.m[6]);
+  mis = or_xor(mis, __ballot(a < b), w.m[7]);
+  return or_xor(mis, __ballot(a < 0.0), w.m[8]);
+}
+
 // M diag (dmax - dmin) and m B diag (dmax - dmin): mp and mbp per u'_0 u'_1 u'_2.
 constexpr double kMScale = kPointModel.M * kPointModel.diag * kImpDelta;
 constexpr double kMBScale = kPointModel.mass * kPointModel.B * kPointModel.diag * kImpDelta;
@@ -657,6 +696,7 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
   uint32_t act = local_edge_mask(c, 0.0, 0.0);
   PieceWeights pw;
   piece_weights(act, pw);
+  EdgeWaves aw;
   const int nstage = 4 * pm.nsub;
 #pragma unroll 20
   for (int e = 0; e < nstage; ++e) {
@@ -686,30 +726,32 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
     if (more) local_collide(L, nex, ney, k, ehi);
     double ux, uy;
     local_piece_min(c, pw, vsx, vsy, &ux, &uy);
-    uint32_t A2 = local_edge_mask(c, ux, uy);
+    uint64_t mis;
     if (e == 0) {
       // The first stage's warm start (every penetrating edge active) is exact
       // for a single contact but wrong for about half of the multi-contact
       // lanes (53 % of all active-set iterations of a step were this stage's):
       // one semismooth Newton step for every lane here, in line.
-      act = A2;
+      act = local_edge_mask(c, ux, uy);
       piece_weights(act, pw);
       local_piece_min(c, pw, vsx, vsy, &ux, &uy);
-      A2 = local_edge_mask(c, ux, uy);
+      edge_waves(act, aw);
     }
-    bool done = A2 == act;
+    mis = edge_mismatch(c, ux, uy, aw);
     LocalSlots cn;
     if (more) local_slots(pm, k, cn);
 #ifdef OGBX_PHYS_STATS
-    if (!done) {
-      const int pc = __builtin_popcount(A2 ^ act);
+    if ((mis >> (threadIdx.x & 63)) & 1u) {
+      const int pc = __builtin_popcount(local_edge_mask(c, ux, uy) ^ act);
       OGBX_STAT(0);
       OGBX_STAT(pc == 1 ? 1 : (pc == 2 ? 2 : 3));
     }
     int trips = 0;
 #endif
-    if (__builtin_expect(__any(!done), 0)) {
+    if (__builtin_expect(mis != 0, 0)) {
       OGBX_WPATH(0);
+      uint32_t A2 = local_edge_mask(c, ux, uy);
+      bool done = A2 == act;
 #pragma unroll 1
       for (int it = 0; it < kLeanIters && !done; ++it) {
         OGBX_WPATH(20);
@@ -724,6 +766,7 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
         done = A2 == act;
       }
       bl |= !done;
+      edge_waves(act, aw);
 #ifdef OGBX_PHYS_STATS
       if (trips == 1) OGBX_STAT(5);
 #endif

@@ -133,6 +133,12 @@ def _bind():
             P(GcDraws), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_void_p, P(GcDrawRecord), ctypes.c_void_p,
         ]
+        L.ogbx_gc_sample_ahead.restype = ctypes.c_int32
+        L.ogbx_gc_sample_ahead.argtypes = [
+            P(GcBuffer), P(GcConfig), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64,
+            ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+        ]
         L.ogbx_gc_traj_end.restype = ctypes.c_int32
         L.ogbx_gc_traj_end.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                        ctypes.c_void_p]
@@ -235,8 +241,10 @@ class GCDataset:
 
     config keys read (as the reference): discount, value_/actor_ p_curgoal,
     p_trajgoal, p_randomgoal, geom_sample, gc_negative, p_aug, frame_stack;
-    and one of this sampler's own: row_record (default True; False skips the
-    interleaved copy of the small columns, ``_row_record``).
+    and two of this sampler's own: row_record (default True; False skips the
+    interleaved copy of the small columns, ``_row_record``) and lookahead
+    (default True; False samples every call in one launch without computing
+    the next call's selectors ahead, ``_launch_plain``).
     """
 
     def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None, _plain=False):
@@ -300,6 +308,11 @@ class GCDataset:
         self._seed = int(seed) if seed is not None else None
         self._calls = 0
         self._out_cache = {}
+        # look-ahead (ogbx_gc_sample_ahead): two ping-pong selector buffers and
+        # the (batch, num_batches, stream, call) whose selectors one of them holds
+        self._lookahead = bool(config.get('lookahead', True))
+        self._ahead_bufs = None
+        self._ahead = None
 
     # ---------------------------------------------------------------- helpers
     _RECORD_MAX = 128  # one L2 line
@@ -416,6 +429,42 @@ class GCDataset:
             add(goal_src, 'actor_goals', 3)
         return out, cols
 
+    _AHEAD_MAX = 1024  # samples per call the look-ahead kernel takes (one per workgroup)
+    _AHEAD_WORDS = 8   # OGBX_GC_AHEAD_WORDS
+    _HGC_AHEAD_WORDS = 20  # OGBX_HGC_AHEAD_WORDS
+
+    def _ahead_slots(self, B, nb, stream, call, words):
+        """(ahead_in, ahead_out, index of ahead_out) for call `call`: the
+        selectors stored by the previous launch when it stored them for exactly
+        this (batch, num_batches, stream, call), else none (computed in line)."""
+        if self._ahead_bufs is None or self._ahead_bufs[0].numel() < self._AHEAD_MAX * words:
+            torch = _torch()
+            self._ahead_bufs = [torch.empty(self._AHEAD_MAX * words, dtype=torch.int64, device=self.device)
+                                for _ in range(2)]
+            self._ahead_ptrs = [t.data_ptr() for t in self._ahead_bufs]
+            self._ahead = None
+        a = self._ahead
+        if a is not None and a[0] == (B, nb, stream, call):
+            return self._ahead_ptrs[a[1]], self._ahead_ptrs[1 - a[1]], 1 - a[1]
+        return None, self._ahead_ptrs[0], 0
+
+    def _launch_plain(self, col_p, ncols, B, nb, seed, call, idx_p, vg_p, ag_p, masks_p, rewards_p, stream):
+        """One Philox-mode GCDataset.sample launch.  Small calls (<= 1024
+        samples) go through the look-ahead kernel: this launch gathers from
+        the selectors the previous equal call stored (when it stored them for
+        exactly this call) and stores the next call's; results are
+        bit-identical either way."""
+        total = B * nb
+        if not self._lookahead or total > self._AHEAD_MAX:
+            self._ahead = None
+            return self._L.ogbx_gc_sample(self._buf, self._cfg, col_p, ncols, B, nb, None, seed, call, idx_p, vg_p,
+                                          ag_p, masks_p, rewards_p, None, stream)
+        src, dst, which = self._ahead_slots(B, nb, stream, call, self._AHEAD_WORDS)
+        st = self._L.ogbx_gc_sample_ahead(self._buf, self._cfg, col_p, ncols, B, nb, seed, call, src, dst, idx_p,
+                                          vg_p, ag_p, masks_p, rewards_p, stream)
+        self._ahead = ((B, nb, stream, call + 1), which) if st == 0 else None
+        return st
+
     def sample(self, batch_size, idxs=None, evaluation=False, draws=None, record_draws=False,
                num_batches=1, _keys=None, out=None):
         """GCDataset.sample (datasets.py:213-294), one fused launch.
@@ -440,9 +489,8 @@ class GCDataset:
             if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
                 col_p, ncols, idx_p, masks_p, rewards_p = hit[2]
                 seed, call = self._next_seed()
-                _lib.check(self._L.ogbx_gc_sample(
-                    self._buf, self._cfg, col_p, ncols, int(batch_size), int(num_batches), None, seed, call,
-                    idx_p, None, None, masks_p, rewards_p, None, _lib.stream_of(self.device)), 'gc_sample')
+                _lib.check(self._launch_plain(col_p, ncols, int(batch_size), int(num_batches), seed, call, idx_p, None,
+                                              None, masks_p, rewards_p, _lib.stream_of(self.device)), 'gc_sample')
                 self._p_aug_draw(out, evaluation)
                 return out
         out, cols = self._columns(total, _keys)
@@ -476,10 +524,16 @@ class GCDataset:
                                     device=self.device) for k in _DRAW_ORDER}
             rec = GcDrawRecord(*[rec_t[k].data_ptr() for k in _DRAW_ORDER])
         seed, call = self._next_seed()
-        _lib.check(self._L.ogbx_gc_sample(
-            self._buf, self._cfg, ctypes.cast(col_arr, ctypes.c_void_p), len(cols), int(batch_size),
-            int(num_batches), dr, seed, call, _lib.ptr(idx_out), _lib.ptr(vg), _lib.ptr(ag), _lib.ptr(masks),
-            _lib.ptr(rewards), rec, _lib.stream_of(self.device)), 'gc_sample')
+        if plain_call:
+            st = self._launch_plain(ctypes.cast(col_arr, ctypes.c_void_p), len(cols), int(batch_size),
+                                    int(num_batches), seed, call, _lib.ptr(idx_out), _lib.ptr(vg), _lib.ptr(ag),
+                                    _lib.ptr(masks), _lib.ptr(rewards), _lib.stream_of(self.device))
+        else:
+            st = self._L.ogbx_gc_sample(
+                self._buf, self._cfg, ctypes.cast(col_arr, ctypes.c_void_p), len(cols), int(batch_size),
+                int(num_batches), dr, seed, call, _lib.ptr(idx_out), _lib.ptr(vg), _lib.ptr(ag), _lib.ptr(masks),
+                _lib.ptr(rewards), rec, _lib.stream_of(self.device))
+        _lib.check(st, 'gc_sample')
         if self._plain:
             out['_idxs'] = idx_out
         else:
@@ -547,6 +601,12 @@ def _bind_hgc():
     L = _bind()
     if not getattr(L, '_hgc_bound', False):
         P = ctypes.POINTER
+        L.ogbx_hgc_sample_ahead.restype = ctypes.c_int32
+        L.ogbx_hgc_sample_ahead.argtypes = [
+            P(GcBuffer), P(GcConfig), P(HgcConfig), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+            ctypes.c_int64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, P(HgcOutputs),
+            ctypes.c_void_p,
+        ]
         L.ogbx_hgc_sample.restype = ctypes.c_int32
         L.ogbx_hgc_sample.argtypes = [
             P(GcBuffer), P(GcConfig), P(HgcConfig), ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
@@ -691,9 +751,18 @@ class HGCDataset(GCDataset):
                     self._out_cache.clear()
                 self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), col_arr, ncols, outs, col_keep)
         seed, call = self._next_seed()
-        _lib.check(self._Lh.ogbx_hgc_sample(
-            self._buf, self._cfg, self._hcfg, col_arr, ncols, int(batch_size),
-            int(num_batches), dr, seed, call, outs, rec, _lib.stream_of(self.device)), 'hgc_sample')
+        stream = _lib.stream_of(self.device)
+        B, nb = int(batch_size), int(num_batches)
+        if plain_call and self._lookahead and B * nb <= self._AHEAD_MAX:
+            src, dst, which = self._ahead_slots(B, nb, stream, call, self._HGC_AHEAD_WORDS)
+            st = self._Lh.ogbx_hgc_sample_ahead(self._buf, self._cfg, self._hcfg, col_arr, ncols, B, nb, seed, call,
+                                                src, dst, outs, stream)
+            self._ahead = ((B, nb, stream, call + 1), which) if st == 0 else None
+        else:
+            self._ahead = None
+            st = self._Lh.ogbx_hgc_sample(self._buf, self._cfg, self._hcfg, col_arr, ncols, B, nb, dr, seed, call,
+                                          outs, rec, stream)
+        _lib.check(st, 'hgc_sample')
         self._p_aug_draw(out, evaluation)
         if record_draws:
             out['_draws'] = rec_t

@@ -287,3 +287,42 @@ def test_row_record_stride_and_in_place_updates(gpu, gold):
     assert bool(hit.all())  # every refilled row is a current dataset row
     chk = gc.sample(512, record_draws=True)
     assert torch.equal(chk['actions'], ds['actions'][chk['_idxs']])
+
+
+def test_lookahead_matches_direct_sampling(gpu, gold):
+    """The look-ahead kernel (ogbx_gc_sample_ahead: call c gathers from the
+    selectors call c-1 stored, and stores call c+1's) returns the batches of
+    direct sampling bit for bit, across out= refills, batch-size changes,
+    interleaved recorded / injected calls (which consume a call index and
+    invalidate the stored selectors), num_batches > 1, and calls above the
+    look-ahead's 1,024-sample limit."""
+    data = orc.load_dataset(_raw(gold), compact_dataset=True)
+    for cname in ('gciql', 'crl'):
+        cfg = dict(CONFIGS[cname], p_aug=None, frame_stack=None)
+        a = GCDataset(Dataset(data, device=gpu), cfg, seed=21)
+        b = GCDataset(Dataset(data, device=gpu), dict(cfg, lookahead=False), seed=21)
+        prev_a = prev_b = None
+        plan = [(1024, 1, 'fresh'), (1024, 1, 'out'), (1024, 1, 'out'), (256, 2, 'fresh'), (256, 2, 'fresh'),
+                (1024, 1, 'record'), (1024, 1, 'fresh'), (1024, 1, 'fresh'), (1000, 2, 'fresh'), (1024, 1, 'fresh'),
+                (64, 1, 'fresh'), (64, 1, 'out')]
+        for i, (B, nb, mode) in enumerate(plan):
+            if mode == 'record':
+                x, y = a.sample(B, record_draws=True), b.sample(B, record_draws=True)
+            elif mode == 'out' and prev_a is not None and prev_a['masks'].numel() == B * nb:
+                x, y = a.sample(B, num_batches=nb, out=prev_a), b.sample(B, num_batches=nb, out=prev_b)
+            else:
+                x, y = a.sample(B, num_batches=nb), b.sample(B, num_batches=nb)
+            for k in y:
+                if not k.startswith('_'):
+                    assert torch.equal(x[k], y[k]), (cname, i, k)
+            if mode != 'record':
+                prev_a, prev_b = x, y
+        assert a._ahead is not None  # the last calls ran ahead
+    # Dataset.sample (plain sampler) and get_random_idxs
+    d1, d2 = Dataset(data, device=gpu), Dataset(data, device=gpu)
+    d2._sampler()._lookahead = False
+    d1._sampler()._seed = d2._sampler()._seed = 5
+    for _ in range(3):
+        x, y = d1.sample(512), d2.sample(512)
+        for k in y:
+            assert torch.equal(x[k], y[k]), k

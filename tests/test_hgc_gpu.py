@@ -57,3 +57,26 @@ def test_hgc_out_reuse(gpu, gold):  # noqa: F811
     assert b2 is a2
     for k in keys:
         assert torch.equal(b1[k], b2[k]), k
+
+
+@pytest.mark.parametrize('cname', list(HGC_CONFIGS))
+def test_hgc_lookahead_matches_direct_sampling(gpu, gold, cname):  # noqa: F811
+    """hgc_ahead_kernel (selectors of call c stored by the launch of call c-1)
+    returns the batches of direct sampling bit for bit, over out= refills,
+    size changes and an interleaved recorded call."""
+    data, _, _, keys = hgc_case(gold, cname, True)
+    a = HGCDataset(Dataset(data, device=gpu), dict(HGC_CONFIGS[cname]), seed=8)
+    b = HGCDataset(Dataset(data, device=gpu), dict(HGC_CONFIGS[cname], lookahead=False), seed=8)
+    prev_a = prev_b = None
+    for i, (B, mode) in enumerate([(1024, 'fresh'), (1024, 'out'), (1024, 'out'), (300, 'fresh'), (300, 'record'),
+                                   (300, 'fresh'), (300, 'fresh'), (2048, 'fresh'), (1024, 'fresh')]):
+        if mode == 'record':
+            x, y = a.sample(B, record_draws=True), b.sample(B, record_draws=True)
+        elif mode == 'out':
+            x, y = a.sample(B, out=prev_a), b.sample(B, out=prev_b)
+        else:
+            x, y = a.sample(B), b.sample(B)
+        for k in keys:
+            assert torch.equal(x[k], y[k]), (i, k)
+        if mode != 'record':
+            prev_a, prev_b = x, y
