@@ -480,6 +480,8 @@ def bench_gcsample(args, world, rank, dev):
     cfg = dict(discount=0.995, value_p_curgoal=0.2, value_p_trajgoal=0.5, value_p_randomgoal=0.3,
                value_geom_sample=True, actor_p_curgoal=0.0, actor_p_trajgoal=1.0, actor_p_randomgoal=0.0,
                actor_geom_sample=False, gc_negative=True, p_aug=0.0, frame_stack=None)
+    if 'OGBX_GC_LOOKAHEAD' in os.environ:  # A/B knob (the sampler's lookahead config key)
+        cfg['lookahead'] = os.environ['OGBX_GC_LOOKAHEAD'] != '0'
     gc = GCDataset(Dataset(data, device=dev), cfg, seed=rank)
     B = 1024
     batch = gc.sample(B)
@@ -553,6 +555,8 @@ def bench_hgcsample(args, world, rank, dev):
     cfg = dict(discount=0.995, value_p_curgoal=0.2, value_p_trajgoal=0.5, value_p_randomgoal=0.3,
                value_geom_sample=True, actor_p_curgoal=0.0, actor_p_trajgoal=1.0, actor_p_randomgoal=0.0,
                actor_geom_sample=False, gc_negative=True, p_aug=0.0, frame_stack=None, subgoal_steps=100)
+    if 'OGBX_GC_LOOKAHEAD' in os.environ:  # A/B knob (the sampler's lookahead config key)
+        cfg['lookahead'] = os.environ['OGBX_GC_LOOKAHEAD'] != '0'
     hgc = HGCDataset(Dataset(data, device=dev), cfg, seed=rank)
     B = 1024
     batch = hgc.sample(B)

@@ -147,8 +147,10 @@ __device__ __forceinline__ void role_tangents(Contacts& c) {
 
 // Integer weights of a mask, per slot: S = a0 + a1 + 2 a2, T = a0 + a1,
 // D = a0 - a1 (as doubles).
+// A2 = a0 + a1 + a2 and C2 = a2 of slot 2 feed the lean loop's double-angle
+// form of the corner terms (local_piece_min).
 struct PieceWeights {
-  double S0, T0, D0, S1, T1, D1, S2, T2, D2;
+  double S0, T0, D0, S1, T1, D1, S2, T2, D2, A2, C2;
 };
 
 __device__ __forceinline__ void piece_weights(uint32_t A, PieceWeights& p) {
@@ -161,6 +163,9 @@ __device__ __forceinline__ void piece_weights(uint32_t A, PieceWeights& p) {
   one(0, p.S0, p.T0, p.D0);
   one(1, p.S1, p.T1, p.D1);
   one(2, p.S2, p.T2, p.D2);
+  const int a2 = (A >> 8) & 1;
+  p.A2 = (double)(((A >> 6) & 1) + ((A >> 7) & 1) + a2);
+  p.C2 = (double)a2;
 }
 
 // a = n.u + kp and b = t.u of slot s.
@@ -536,31 +541,30 @@ __device__ __forceinline__ double kp_or_far(bool on, double kp) {
 }
 
 // Normal-equation solve of the piece with weights p (local role layout).
+// The corner slot's terms use the double-angle form: with c2 = nx^2 - ny^2,
+// s2 = 2 nx ny (nx^2 + ny^2 = 1 to an ulp), S nn' + T tt' + D (nt' + tn') =
+// (a0+a1+a2) I + [a2 c2 + (a1-a0) s2] diag(1, -1) + [a2 s2 - (a1-a0) c2] offdiag
+// (a_e the edge activities; PieceWeights carries A2 = a0+a1+a2 and C2 = a2).
 __device__ __forceinline__ void local_piece_min(const LocalSlots& c, const PieceWeights& p, double vx, double vy,
                                                 double* ux, double* uy) {
 #pragma clang fp contract(fast)
   const double w0 = c.w0, w1 = c.w1, w2 = c.w2;
-  double h00 = c.mp + w0 * p.S0 + w1 * p.T1;
-  double h11 = c.mp + w0 * p.T0 + w1 * p.S1;
-  double h01 = w0 * p.D0 - w1 * p.D1;
+  const double nx = c.nx2, ny = c.ny2;
+  const double c2 = fma(nx, nx, -(ny * ny)), s2 = (nx + nx) * ny;
+  const double A = w2 * p.A2, B = w2 * p.D2, C = w2 * p.C2;  // B = -(a1 - a0) w2
+  const double X = fma(C, c2, -(B * s2));
+  const double mpA = c.mp + A;
+  double h00 = fma(w0, p.S0, fma(w1, p.T1, mpA)) + X;
+  double h11 = fma(w0, p.T0, fma(w1, p.S1, mpA)) - X;
+  double h01 = fma(w0, p.D0, -(w1 * p.D1));
+  h01 = fma(C, s2, h01);
+  h01 = fma(B, c2, h01);
   const double g0 = w0 * c.kp0, g1 = w1 * c.kp1;
   double r0 = c.mbp * vx + g0 * p.S0 - g1 * p.D1;
   double r1 = c.mbp * vy + g0 * p.D0 + g1 * p.S1;
-  const double nx = c.nx2, ny = c.ny2;
-  const double q = nx * nx, s = ny * ny, o = nx * ny;
-  const double WS = w2 * p.S2, WT = w2 * p.T2, WD = w2 * p.D2;
-  const double t = WD * o;
-  h00 = fma(WS, q, h00);  // (chained: one fma per term, no partial sums)
-  h00 = fma(WT, s, h00);
-  h00 = fma(-2.0, t, h00);
-  h11 = fma(WS, s, h11);
-  h11 = fma(WT, q, h11);
-  h11 = fma(2.0, t, h11);
-  h01 = fma(WS - WT, o, h01);
-  h01 = fma(WD, q - s, h01);
-  const double k2 = c.kp2;
-  r0 -= k2 * (WS * nx - WD * ny);
-  r1 -= k2 * (WS * ny + WD * nx);
+  const double WS = A + C, k2 = c.kp2;
+  r0 -= k2 * (WS * nx - B * ny);
+  r1 -= k2 * (WS * ny + B * nx);
   const double idet = fast_recip(h00 * h11 - h01 * h01);
   *ux = (h11 * r0 - h01 * r1) * idet;
   *uy = (h00 * r1 - h01 * r0) * idet;
@@ -576,45 +580,6 @@ __device__ __forceinline__ uint32_t local_edge_mask(const LocalSlots& c, double 
   const double b = c.nx2 * uy - c.ny2 * ux;
   m |= (a < -b ? 64u : 0u) | (a < b ? 128u : 0u) | (a < 0.0 ? 256u : 0u);
   return m;
-}
-
-// The active set as nine wave masks (bit l of m[e]: edge e of lane l is
-// active): the stage's consistency check then runs on the scalar unit -- each
-// edge test's v_cmp result IS a wave mask -- instead of packing nine
-// per-lane bits with v_cndmask / v_or3.
-struct EdgeWaves {
-  uint64_t m[9];
-};
-
-__device__ __forceinline__ void edge_waves(uint32_t act, EdgeWaves& w) {
-#pragma unroll
-  for (int e = 0; e < 9; ++e) w.m[e] = __ballot((act >> e) & 1u);
-}
-
-// acc | (m ^ a) on the scalar unit: two SALU ops (written out: LLVM turns the
-// OR of XORs into nine compare-and-select triples).
-__device__ __forceinline__ uint64_t or_xor(uint64_t acc, uint64_t m, uint64_t a) {
-  uint64_t x;
-  asm("s_xor_b64 %0, %1, %2\n\ts_or_b64 %0, %0, %3" : "=&s"(x) : "s"(m), "s"(a), "s"(acc) : "scc");
-  return x;
-}
-
-// Lanes whose edge mask at U differs from the active set w (local_edge_mask's
-// tests, bit for bit).
-__device__ __forceinline__ uint64_t edge_mismatch(const LocalSlots& c, double ux, double uy, const EdgeWaves& w) {
-#pragma clang fp contract(fast)
-  const double P = ux + uy, Q = ux - uy;
-  const double a = c.nx2 * ux + (c.ny2 * uy + c.kp2);
-  const double b = c.nx2 * uy - c.ny2 * ux;
-  uint64_t mis = __ballot(c.kp0 < P) ^ w.m[0];
-  mis = or_xor(mis, __ballot(c.kp0 < Q), w.m[1]);
-  mis = or_xor(mis, __ballot(c.kp0 < ux), w.m[2]);
-  mis = or_xor(mis, __ballot(c.kp1 < -Q), w.m[3]);
-  mis = or_xor(mis, __ballot(c.kp1 < P), w.m[4]);
-  mis = or_xor(mis, __ballot(c.kp1 < uy), w.m[5]);
-  mis = or_xor(mis, __ballot(a < -b), w.m[6]);
-  mis = or_xor(mis, __ballot(a < b), w.m[7]);
-  return or_xor(mis, __ballot(a < 0.0), w.m[8]);
 }
 
 // M diag (dmax - dmin) and m B diag (dmax - dmin): mp and mbp per u'_0 u'_1 u'_2.
@@ -696,7 +661,6 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
   uint32_t act = local_edge_mask(c, 0.0, 0.0);
   PieceWeights pw;
   piece_weights(act, pw);
-  EdgeWaves aw;
   const int nstage = 4 * pm.nsub;
 #pragma unroll 20
   for (int e = 0; e < nstage; ++e) {
@@ -726,32 +690,30 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
     if (more) local_collide(L, nex, ney, k, ehi);
     double ux, uy;
     local_piece_min(c, pw, vsx, vsy, &ux, &uy);
-    uint64_t mis;
+    uint32_t A2 = local_edge_mask(c, ux, uy);
     if (e == 0) {
       // The first stage's warm start (every penetrating edge active) is exact
       // for a single contact but wrong for about half of the multi-contact
       // lanes (53 % of all active-set iterations of a step were this stage's):
       // one semismooth Newton step for every lane here, in line.
-      act = local_edge_mask(c, ux, uy);
+      act = A2;
       piece_weights(act, pw);
       local_piece_min(c, pw, vsx, vsy, &ux, &uy);
-      edge_waves(act, aw);
+      A2 = local_edge_mask(c, ux, uy);
     }
-    mis = edge_mismatch(c, ux, uy, aw);
+    bool done = A2 == act;
     LocalSlots cn;
     if (more) local_slots(pm, k, cn);
 #ifdef OGBX_PHYS_STATS
-    if ((mis >> (threadIdx.x & 63)) & 1u) {
-      const int pc = __builtin_popcount(local_edge_mask(c, ux, uy) ^ act);
+    if (!done) {
+      const int pc = __builtin_popcount(A2 ^ act);
       OGBX_STAT(0);
       OGBX_STAT(pc == 1 ? 1 : (pc == 2 ? 2 : 3));
     }
     int trips = 0;
 #endif
-    if (__builtin_expect(mis != 0, 0)) {
+    if (__builtin_expect(__any(!done), 0)) {
       OGBX_WPATH(0);
-      uint32_t A2 = local_edge_mask(c, ux, uy);
-      bool done = A2 == act;
 #pragma unroll 1
       for (int it = 0; it < kLeanIters && !done; ++it) {
         OGBX_WPATH(20);
@@ -766,7 +728,6 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
         done = A2 == act;
       }
       bl |= !done;
-      edge_waves(act, aw);
 #ifdef OGBX_PHYS_STATS
       if (trips == 1) OGBX_STAT(5);
 #endif

@@ -243,8 +243,8 @@ class GCDataset:
     p_trajgoal, p_randomgoal, geom_sample, gc_negative, p_aug, frame_stack;
     and two of this sampler's own: row_record (default True; False skips the
     interleaved copy of the small columns, ``_row_record``) and lookahead
-    (default True; False samples every call in one launch without computing
-    the next call's selectors ahead, ``_launch_plain``).
+    (True: each call also computes the next equal call's selectors,
+    ``_launch_plain``; default False for GCDataset, True for HGCDataset).
     """
 
     def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None, _plain=False):
@@ -310,7 +310,7 @@ class GCDataset:
         self._out_cache = {}
         # look-ahead (ogbx_gc_sample_ahead): two ping-pong selector buffers and
         # the (batch, num_batches, stream, call) whose selectors one of them holds
-        self._lookahead = bool(config.get('lookahead', True))
+        self._lookahead = bool(config.get('lookahead', self._LOOKAHEAD_DEFAULT))
         self._ahead_bufs = None
         self._ahead = None
 
@@ -430,6 +430,10 @@ class GCDataset:
         return out, cols
 
     _AHEAD_MAX = 1024  # samples per call the look-ahead kernel takes (one per workgroup)
+    # GC: measured neutral (5.99 vs 5.94 us per B = 1,024 call: the stored
+    # selectors' load costs about what the short GC draw chain did), so off by
+    # default; HGC's longer chain gains (8.05 vs 8.38 us), on by default
+    _LOOKAHEAD_DEFAULT = False
     _AHEAD_WORDS = 8   # OGBX_GC_AHEAD_WORDS
     _HGC_AHEAD_WORDS = 20  # OGBX_HGC_AHEAD_WORDS
 
@@ -638,6 +642,8 @@ class HGCDataset(GCDataset):
     low_subgoal_steps, low_discount.  One fused launch of hgc_sample_kernel
     per sample() returns the reference's 27 (28 with low_discount) keys.
     """
+
+    _LOOKAHEAD_DEFAULT = True
 
     def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None):
         super().__init__(dataset, config, preprocess_frame_stack=preprocess_frame_stack, seed=seed)

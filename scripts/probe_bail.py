@@ -38,6 +38,8 @@ L.ogbx_diag_phys_stats(buf)
 s = list(buf)
 print(f'bench 300 steps: contact wave-stages {s[9]} bail waves {s[14]} slow wave-stages {s[12]} '
       f'iterating wave-stages {s[13]} band wave-stages {s[10]}', flush=True)
+print(f'  lean loop: lane mismatches {s[0]} (1 edge {s[1]}, 2 edges {s[2]}, more {s[3]}), '
+      f'iterations {s[4]}, single-trip fixes {s[5]}', flush=True)
 print(f'  lanes iterating {s[0]}: new contact {s[1]}, friction edge {s[2]}, normal edge {s[3]}; '
       f'trips {s[4]}, settled in one trip {s[5]}; by RK stage 0/1/2: {s[6]} {s[7]} {s[8]}', flush=True)
 print(f'  flipping-edge |residual| max: <1e-12 {s[16]}, <1e-9 {s[17]}, <1e-6 {s[18]}, <1e-3 {s[19]}, larger {s[20]}',

@@ -299,7 +299,7 @@ def test_lookahead_matches_direct_sampling(gpu, gold):
     data = orc.load_dataset(_raw(gold), compact_dataset=True)
     for cname in ('gciql', 'crl'):
         cfg = dict(CONFIGS[cname], p_aug=None, frame_stack=None)
-        a = GCDataset(Dataset(data, device=gpu), cfg, seed=21)
+        a = GCDataset(Dataset(data, device=gpu), dict(cfg, lookahead=True), seed=21)
         b = GCDataset(Dataset(data, device=gpu), dict(cfg, lookahead=False), seed=21)
         prev_a = prev_b = None
         plan = [(1024, 1, 'fresh'), (1024, 1, 'out'), (1024, 1, 'out'), (256, 2, 'fresh'), (256, 2, 'fresh'),
@@ -320,7 +320,7 @@ def test_lookahead_matches_direct_sampling(gpu, gold):
         assert a._ahead is not None  # the last calls ran ahead
     # Dataset.sample (plain sampler) and get_random_idxs
     d1, d2 = Dataset(data, device=gpu), Dataset(data, device=gpu)
-    d2._sampler()._lookahead = False
+    d1._sampler()._lookahead, d2._sampler()._lookahead = True, False
     d1._sampler()._seed = d2._sampler()._seed = 5
     for _ in range(3):
         x, y = d1.sample(512), d2.sample(512)

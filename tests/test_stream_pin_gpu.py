@@ -31,7 +31,7 @@ pytestmark = pytest.mark.gpu
 
 STREAM_VERSION = 2
 PINNED = {
-    'pointmaze': None,  # recorded below
+    'pointmaze': '86126b859d3c30f41d8249ec',
     'powder_easy': '408325547e866809b750a981',
     'powder_medium': 'd1d796b7afa8af8c9738fe06',
     'gc_sample': 'bf2b89ee32edf7c0e11c4556',
