@@ -558,6 +558,7 @@ def bench_hgcsample(args, world, rank, dev):
     if 'OGBX_GC_LOOKAHEAD' in os.environ:  # A/B knob (the sampler's lookahead config key)
         cfg['lookahead'] = os.environ['OGBX_GC_LOOKAHEAD'] != '0'
     hgc = HGCDataset(Dataset(data, device=dev), cfg, seed=rank)
+    hgc_kernel = 'hgc_ahead_kernel' if hgc._lookahead else 'hgc_sample_kernel'  # the launch of a steady call
     B = 1024
     batch = hgc.sample(B)
 
@@ -594,9 +595,9 @@ def bench_hgcsample(args, world, rank, dev):
         config=dict(workload='humanoidmaze-large-navigate-v0 offline replay (HIQL sampler)', rows=R, batch=B,
                     agent_config='hiql humanoid (discount 0.995, subgoal_steps 100)',
                     parallelism=f'replica x{world}'),
-        roofline=dict(bound='latency', kernel='hgc_sample_kernel', achieved=achieved, peak=HBM_PEAK_GBS,
+        roofline=dict(bound='latency', kernel=hgc_kernel, achieved=achieved, peak=HBM_PEAK_GBS,
                       unit='GB/s', frac=achieved / HBM_PEAK_GBS,
-                      traffic=_traffic('hgc_sample_kernel', 'hgcsample', B, world),
+                      traffic=_traffic(hgc_kernel, 'hgcsample', B, world),
                       kernel_ms=kern_ms, **kern_info, alg_bytes_per_launch=per_sample * B),
         extra=extra,
     )
