@@ -807,6 +807,23 @@ struct FullWorld {
     const uint32_t ec = re < 0.05f ? 0u : (re < 0.4f ? 1u : 2u);
     return b | (ic << 7) | (ec << 10);
   }
+  // The same 12 bits straight from the three Philox words (u01f_from(w) =
+  // (w >> 8) 2^-24, so each decision is a threshold on the word): with rm in
+  // [0, 1), bits 1-6 are the constants 0 | rm>.5 | 1 | fl(fl(rm - 2) + 2) > .5
+  // | 1 | 1, and every threshold below is where the float32 decision of
+  // rand_bits switches (tests/test_powder_rand_bits.py checks all 2^24
+  // words of each field against rand_bits).  Eight integer compares per cell
+  // instead of three conversions and twenty float operations.
+  static constexpr uint32_t kRmHalf = 8388609u << 8, kRmHalfR = 8388610u << 8;
+  static constexpr uint32_t kRiT0 = 335545u << 8, kRiT1 = 838861u << 8, kRiT2 = 3355444u << 8, kRiT3 = 5033165u << 8;
+  static constexpr uint32_t kReT0 = 838861u << 8, kReT1 = 6710887u << 8;
+  __device__ static __forceinline__ uint32_t rand_bits_w(uint32_t wm, uint32_t wi, uint32_t we) {
+    const uint32_t b = 0x68u | (wm >= kRmHalf ? 0x5u : 0u) | (wm >= kRmHalfR ? 0x10u : 0u);
+    const uint32_t ic = (uint32_t)(wi >= kRiT0) + (uint32_t)(wi >= kRiT1) + (uint32_t)(wi >= kRiT2) +
+                        (uint32_t)(wi >= kRiT3);
+    const uint32_t ec = (uint32_t)(we >= kReT0) + (uint32_t)(we >= kReT1);
+    return b | (ic << 7) | (ec << 10);
+  }
   static constexpr uint32_t kRi002 = 1, kRi005 = 2, kRi02 = 3, kRi03 = 4, kRe005 = 1, kRe04 = 2;
   __device__ __forceinline__ bool ri_lt(int k, uint32_t cat) const { return ((s.rb[cell(k)] >> 7) & 7u) < cat; }
   __device__ __forceinline__ bool re_lt(int k, uint32_t cat) const { return ((s.rb[cell(k)] >> 10) & 3u) < cat; }
@@ -842,7 +859,7 @@ struct FullWorld {
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        s.rb[cell(q + j * G)] = (uint16_t)rand_bits(u01f_from(w[3 * j]), u01f_from(w[3 * j + 1]), u01f_from(w[3 * j + 2]));
+        s.rb[cell(q + j * G)] = (uint16_t)rand_bits_w(w[3 * j], w[3 * j + 1], w[3 * j + 2]);
     }
   }
 
