@@ -234,6 +234,11 @@ ogbx_status ogbx_maze_rollout_until_done(ogbx_maze_t env, const void* action, in
 ogbx_status ogbx_maze_state(ogbx_maze_t env, double** qpos, double** goal_xy, int32_t** elapsed,
                             int32_t** task_id, uint32_t** episode);
 
+/* The seed later steps key their Philox draws with (auto-reset, noise), as
+ * the last ogbx_maze_reset set it: a state restored through ogbx_maze_state
+ * into another handle restores its seed with this (checkpoint/restore). */
+ogbx_status ogbx_maze_set_seed(ogbx_maze_t env, uint64_t seed);
+
 /* Free-standing physics: advance `n` point masses one PointEnv step without
  * any env bookkeeping: qpos_out = mj_step^5(qpos + 0.2*action).  Used by the
  * parity tests for arbitrary (qpos, action) pairs.  Replaces point.py:68-73. */
@@ -558,12 +563,21 @@ ogbx_status ogbx_powder_step(ogbx_powder_t env, const int32_t* action, int32_t k
 /* Device pointers to the state: world uint8 [N, H*W] (id | GravityInter<<5 |
  * DidGravity<<6), ctrl int32 [N] (stage | elem<<2 | x<<8 | task<<16),
  * elapsed int32 [N], episode uint32 [N] (Philox counter word, as for
- * ogbx_maze_state).  Writable (state restore). */
+ * ogbx_maze_state).  Any argument may be NULL.  Writable (state restore):
+ * medium/hard envs keep a render cache of the world's colours, and asking for
+ * `world` marks it stale, so the next ogbx_powder_step renders from the state
+ * (write through the pointer before that step, not after it). */
 ogbx_status ogbx_powder_state(ogbx_powder_t env, uint8_t** world, int32_t** ctrl,
                               int32_t** elapsed, uint32_t** episode);
 
+/* The seed of the steps' Philox draws (invalid-action replacements, rand
+ * fields, auto-resets), as the last ogbx_powder_reset set it; restores it with
+ * a state loaded through ogbx_powder_state (checkpoint/restore). */
+ogbx_status ogbx_powder_set_seed(ogbx_powder_t env, uint64_t seed);
+
 /* Medium/hard state: momentum int8 [N, H*W] (channel 6), velocity float32
- * [N, H*W, 2] (channels 3, 4), goal ids uint8 [N, H*W] (cur_goal_world). */
+ * [N, H*W, 2] (channels 3, 4), goal ids uint8 [N, H*W] (cur_goal_world).
+ * Asking for `velocity` marks the render cache stale, as `world` does above. */
 ogbx_status ogbx_powder_full_state(ogbx_powder_t env, int8_t** momentum, float** velocity,
                                    uint8_t** goal_ids);
 

@@ -95,6 +95,7 @@ _SIGNATURES = {
         [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     'ogbx_maze_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p)]),
+    'ogbx_maze_set_seed': (c_int32, [c_void_p, c_uint64]),
     'ogbx_point_physics': (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int64, c_void_p, c_void_p, c_void_p]),
     'ogbx_maze_xy_to_ij': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     'ogbx_maze_ij_to_xy': (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
@@ -118,6 +119,7 @@ _SIGNATURES = {
          c_int32, c_void_p],
     ),
     'ogbx_powder_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p)]),
+    'ogbx_powder_set_seed': (c_int32, [c_void_p, c_uint64]),
     'ogbx_powder_full_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p)]),
     'ogbx_powder_forward': (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     'ogbx_powder_forward_full': (

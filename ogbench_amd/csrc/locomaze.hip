@@ -1004,6 +1004,12 @@ ogbx_status ogbx_maze_state(ogbx_maze_t e, double** qpos, double** goal_xy, int3
   return OGBX_OK;
 }
 
+ogbx_status ogbx_maze_set_seed(ogbx_maze_t e, uint64_t seed) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  e->seed = seed;
+  return OGBX_OK;
+}
+
 ogbx_status ogbx_point_physics(ogbx_maze_t e, const double* qpos_in, const void* action,
                                int32_t action_is_f64, int64_t n, double* qpos_out,
                                uint8_t* contact_out, void* stream) {

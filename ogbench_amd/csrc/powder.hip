@@ -99,6 +99,10 @@ struct PowderState {
   int8_t* mom;       // [N, H*W] fluid momentum (channel 6)
   float2* vel;       // [N, H*W] velocity (channels 3, 4)
   uint8_t* goal_env; // [N, H*W] goal ids (the goal replay is stochastic)
+  // render cache: colour of every cell as of the last state write (R | G << 8,
+  // B), so a render-only step reads 3 bytes per cell instead of id + velocity
+  uint16_t* crg;     // [N, H*W]
+  uint8_t* cb;       // [N, H*W]
 };
 
 template <int WS>
@@ -638,7 +642,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   for (int k = 0; k < FW<WS>::CPT; ++k) S.goal_env[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
   fw.store(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
   const int errs = fw.errors();
-  fw.observe(obs + (size_t)e * C * 6, 0, 0u, 0, Pp->brush);
+  fw.observe(obs + (size_t)e * C * 6, 0, 0u, 0, Pp->brush, false, S.crg + (size_t)e * C, S.cb + (size_t)e * C);
   if (threadIdx.x == 0) {
     S.ctrl[e] = (task << 16) | (errs < Pp->tol_task[task - 1] ? kCtrlSuccess : 0);
     S.elapsed[e] = 0;
@@ -655,7 +659,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     const int32_t* __restrict__ draws, const float* __restrict__ rand, int32_t k_steps, uint8_t* __restrict__ obs,
     float* __restrict__ reward, uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated,
     uint8_t* __restrict__ success, int32_t auto_reset, uint32_t k0, uint32_t k1, uint32_t a0, uint32_t a1,
-    uint32_t r0, uint32_t r1, const uint8_t* __restrict__ skip) {
+    uint32_t r0, uint32_t r1, const uint8_t* __restrict__ skip, int32_t refresh) {
   constexpr int C = WS * WS, CPT = FW<WS>::CPT;
   __shared__ PwFullShared<WS> sh;
   FW<WS> fw(sh);
@@ -740,7 +744,10 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     }
     ctrl = stage | (elem << 2) | (x << 8) | (ctrl & (255 << 16)) | (succ ? kCtrlSuccess : 0);
     const uint32_t acol = sh.lut[sh.elem_ids[elem & 7] & 31];
-    fw.observe(obs + (size_t)o * C * 6, stage, acol, x * grid, brush);
+    // the last step's render also refreshes the cache if the state changed
+    const bool cache = k == k_steps - 1 && (dirty || refresh);
+    fw.observe(obs + (size_t)o * C * 6, stage, acol, x * grid, brush, false, cache ? S.crg + (size_t)e * C : nullptr,
+               cache ? S.cb + (size_t)e * C : nullptr);
   }
   if (dirty) fw.store(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
   if (goal_dirty) {
@@ -757,20 +764,24 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
 // Render-only steps of medium/hard worlds (one step per launch).  An env at
 // stage 0 or 1 of the 3-step action machine that does not auto-reset this step
 // runs no forward: it draws its sub-action, advances the stage and renders its
-// unchanged world (powderworld_env.py:354-427, 462-476).  That needs 9 of the
-// 11 state bytes per cell and writes no state back, but inside
-// pwf_step_kernel it would hold the full rule set's 116 KB of LDS, i.e. one
-// env per CU with nothing to overlap its HBM round trips.  This kernel steps
-// those envs with a 24 KB staging buffer (6 envs per CU) and marks them in
-// `handled`; pwf_step_kernel, launched after it, skips the marked envs.  The
-// predicate is evaluated on the pre-step state by this kernel alone.
+// unchanged world (powderworld_env.py:354-427, 462-476).  Its colours come from
+// the env's render cache (3 bytes per cell, written by the kernel that last
+// changed the state), so the step moves 3 + 6 bytes per cell; inside
+// pwf_step_kernel it would hold the full rule set's 78 KB of LDS, i.e. two
+// envs per CU with little to overlap their HBM round trips.  This kernel steps
+// those envs with a 24 KB staging buffer and marks them in `handled`;
+// pwf_step_kernel, launched after it, skips the marked envs.  The predicate is
+// evaluated on the pre-step state by this kernel alone.  refresh (the cache
+// may be stale, ogbx_powder_env::cache_stale): render from id + velocity as
+// the forward kernels do and rewrite the cache.
 template <int WS>
 __global__ void __launch_bounds__(256) pwf_light_step_kernel(
     const PowderParams* __restrict__ Pp, PowderState S, const int32_t* __restrict__ action,
     const int32_t* __restrict__ draws, uint8_t* __restrict__ obs, float* __restrict__ reward,
     uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated, uint8_t* __restrict__ success,
-    int32_t auto_reset, uint32_t a0, uint32_t a1, uint8_t* __restrict__ handled) {
+    int32_t auto_reset, uint32_t a0, uint32_t a1, uint8_t* __restrict__ handled, int32_t refresh) {
   constexpr int C = WS * WS, CPT = C / 256;
+  static_assert(CPT == 16 || CPT == 4, "64x64 or 32x32 worlds");
   __shared__ alignas(16) uint16_t st[C * 3];  // 6 observation bytes per cell
   __shared__ uint32_t lut[32];
   const int64_t e = blockIdx.x;
@@ -808,29 +819,56 @@ __global__ void __launch_bounds__(256) pwf_light_step_kernel(
   const int rx = x * Pp->grid, brush = Pp->brush;
   // thread t: cells [t*CPT, t*CPT + CPT) of one row
   const int c0 = t * CPT;
-  const uint8_t* wa = S.world + (size_t)e * C + c0;
-  const float4* wv = reinterpret_cast<const float4*>(S.vel + (size_t)e * C + c0);
-  uint8_t ids[CPT];
-  if constexpr (CPT == 16) {
-    const uint4 q = *reinterpret_cast<const uint4*>(wa);
-    const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+  uint32_t col[CPT];  // R | G << 8 | B << 16 per cell
+  uint16_t* crg = S.crg + (size_t)e * C + c0;
+  uint8_t* cb = S.cb + (size_t)e * C + c0;
+  if (!refresh) {
+    // CPT x (2 + 1) bytes: 16 cells = two 16-byte + one 16-byte load, 4 cells = 8 + 4
+    uint32_t g[CPT / 2], b[CPT / 4];
+    if constexpr (CPT == 16) {
+      const uint4 g0 = reinterpret_cast<const uint4*>(crg)[0], g1 = reinterpret_cast<const uint4*>(crg)[1];
+      const uint4 b0 = *reinterpret_cast<const uint4*>(cb);
+      g[0] = g0.x, g[1] = g0.y, g[2] = g0.z, g[3] = g0.w, g[4] = g1.x, g[5] = g1.y, g[6] = g1.z, g[7] = g1.w;
+      b[0] = b0.x, b[1] = b0.y, b[2] = b0.z, b[3] = b0.w;
+    } else {
+      const uint2 g0 = *reinterpret_cast<const uint2*>(crg);
+      g[0] = g0.x, g[1] = g0.y;
+      b[0] = *reinterpret_cast<const uint32_t*>(cb);
+    }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) ids[k] = (uint8_t)(w4[k >> 2] >> (8 * (k & 3)));
+    for (int k = 0; k < CPT; ++k)
+      col[k] = ((g[k >> 1] >> (16 * (k & 1))) & 0xffffu) | (((b[k >> 2] >> (8 * (k & 3))) & 0xffu) << 16);
   } else {
-    const uint32_t q = *reinterpret_cast<const uint32_t*>(wa);
+    const uint8_t* wa = S.world + (size_t)e * C + c0;
+    const float4* wv = reinterpret_cast<const float4*>(S.vel + (size_t)e * C + c0);
+    uint8_t ids[CPT];
+    if constexpr (CPT == 16) {
+      const uint4 q = *reinterpret_cast<const uint4*>(wa);
+      const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int k = 0; k < CPT; ++k) ids[k] = (uint8_t)(q >> (8 * k));
+      for (int k = 0; k < 16; ++k) ids[k] = (uint8_t)(w4[k >> 2] >> (8 * (k & 3)));
+    } else {
+      const uint32_t q = *reinterpret_cast<const uint32_t*>(wa);
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) ids[k] = (uint8_t)(q >> (8 * k));
+    }
+    float4 vv[CPT / 2];
+#pragma unroll
+    for (int k = 0; k < CPT / 2; ++k) vv[k] = wv[k];
+    __syncthreads();  // lut
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const float2 v = (k & 1) ? make_float2(vv[k >> 1].z, vv[k >> 1].w) : make_float2(vv[k >> 1].x, vv[k >> 1].y);
+      col[k] = pw_rgb(lut, fid(ids[k]), v);
+      crg[k] = (uint16_t)(col[k] & 0xffffu);
+      cb[k] = (uint8_t)(col[k] >> 16);
+    }
   }
-  float4 vv[CPT / 2];
-#pragma unroll
-  for (int k = 0; k < CPT / 2; ++k) vv[k] = wv[k];
-  __syncthreads();  // lut
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
-    const int i = c0 + k, col = i % WS;
-    const float2 v = (k & 1) ? make_float2(vv[k >> 1].z, vv[k >> 1].w) : make_float2(vv[k >> 1].x, vv[k >> 1].y);
-    const uint32_t c = pw_rgb(lut, fid(ids[k]), v);
-    const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
+    const int i = c0 + k, cc = i % WS;
+    const uint32_t c = col[k];
+    const bool fr = stage == 1 || (stage == 2 && cc >= rx && cc < rx + brush);
     const uint32_t px = fr ? acol : 0u;
     st[3 * i] = (uint16_t)(c & 0xffffu);
     st[3 * i + 1] = (uint16_t)(((c >> 16) & 0xffu) | ((px & 0xffu) << 8));
@@ -1062,6 +1100,11 @@ struct ogbx_powder_env {
   uint8_t* goals = nullptr;  // easy: [num_tasks, H*W] goal ids
   uint8_t* handled = nullptr;  // medium/hard: [N] env stepped by pwf_light_step_kernel this launch
   bool light = true;           // split render-only steps into pwf_light_step_kernel
+  // the render cache (S.crg / S.cb) may disagree with the state: set at create
+  // and whenever a world or velocity pointer is handed out (the caller may
+  // write through it); the next step then renders from the state and rewrites
+  // the cache of every env
+  bool cache_stale = true;
   uint64_t seed = 0;
   bool was_reset = false;
 };
@@ -1186,6 +1229,8 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
     if (h == hipSuccess) h = hipMalloc(&e->S.mom, n * HW);
     if (h == hipSuccess) h = hipMalloc(&e->S.vel, n * HW * sizeof(float2));
     if (h == hipSuccess) h = hipMalloc(&e->S.goal_env, n * HW);
+    if (h == hipSuccess) h = hipMalloc(&e->S.crg, n * HW * sizeof(uint16_t));
+    if (h == hipSuccess) h = hipMalloc(&e->S.cb, n * HW);
     if (h == hipSuccess) h = hipMalloc(&e->handled, n);
     if (const char* v = std::getenv("OGBX_PWF_LIGHT")) e->light = std::atoi(v) != 0;  // A/B knob
     if (h == hipSuccess) h = hipMemset(e->S.mom, 0, n * HW);
@@ -1218,6 +1263,8 @@ ogbx_status ogbx_powder_destroy(ogbx_powder_t e) {
   (void)hipFree(e->S.mom);
   (void)hipFree(e->S.vel);
   (void)hipFree(e->S.goal_env);
+  (void)hipFree(e->S.crg);
+  (void)hipFree(e->S.cb);
   (void)hipFree(e->goals);
   (void)hipFree(e->handled);
   delete e;
@@ -1288,13 +1335,14 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
     const bool light = e->light && k_steps == 1;
     if (light) {
       PW_LAUNCH(pwf_light_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, action, draws, obs, reward,
-                terminated, truncated, success, auto_reset, a0, a1, e->handled);
+                terminated, truncated, success, auto_reset, a0, a1, e->handled, (int32_t)e->cache_stale);
       OGBX_LAUNCHED("pwf_light_step_kernel");
     }
     PWF_LAUNCH(pwf_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps, obs,
               reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1, r0, r1,
-              light ? e->handled : (const uint8_t*)nullptr);
+              light ? e->handled : (const uint8_t*)nullptr, (int32_t)e->cache_stale);
     OGBX_LAUNCHED("pwf_step_kernel");
+    e->cache_stale = false;  // every env's cache was written by one of the two kernels
   } else {
     PW_LAUNCH(pw_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs,
               reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1);
@@ -1307,10 +1355,17 @@ ogbx_status ogbx_powder_state(ogbx_powder_t e, uint8_t** world, int32_t** ctrl, 
                               uint32_t** episode) {
   OGBX_CHECK(e, OGBX_EINVAL, "null handle");
   if (world) *world = e->S.world;
+  if (world) e->cache_stale = true;
   if (ctrl) *ctrl = e->S.ctrl;
   if (elapsed) *elapsed = e->S.elapsed;
   if (episode) *episode = e->S.episode;
   e->was_reset = true;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_powder_set_seed(ogbx_powder_t e, uint64_t seed) {
+  OGBX_CHECK(e, OGBX_EINVAL, "null handle");
+  e->seed = seed;
   return OGBX_OK;
 }
 
@@ -1319,6 +1374,7 @@ ogbx_status ogbx_powder_full_state(ogbx_powder_t e, int8_t** momentum, float** v
   OGBX_CHECK(e->full, OGBX_EINVAL, "easy worlds carry no momentum / velocity / per-env goals");
   if (momentum) *momentum = e->S.mom;
   if (velocity) *velocity = reinterpret_cast<float*>(e->S.vel);
+  if (velocity) e->cache_stale = true;
   if (goal_ids) *goal_ids = e->S.goal_env;
   return OGBX_OK;
 }

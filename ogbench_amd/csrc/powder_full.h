@@ -933,9 +933,11 @@ struct FullWorld {
 
   // Observation: RGB of the world + action frame (powderworld_env.py:462-476),
   // staged in LDS (6 bytes per cell as three 16-bit stores) and written as
-  // 16-byte stores.  rgb_only: 3 channels.
+  // 16-byte stores.  rgb_only: 3 channels.  crg / cb: also write every cell's
+  // colour to the env's render cache (R | G << 8, B).
   __device__ __forceinline__ void observe(uint8_t* __restrict__ dst, int stage, uint32_t acol, int rx, int brush,
-                                          bool rgb_only = false) const {
+                                          bool rgb_only = false, uint16_t* __restrict__ crg = nullptr,
+                                          uint8_t* __restrict__ cb = nullptr) const {
     fence_idx();
     const bool fr = stage == 1 || (stage == 2 && col >= rx && col < rx + brush);
     const uint32_t px = fr ? acol : 0u;
@@ -945,6 +947,10 @@ struct FullWorld {
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
       const uint32_t c = rgb(fid(s.a[i]), s.v[i]);
+      if (crg != nullptr) {
+        crg[i] = (uint16_t)(c & 0xffffu);
+        cb[i] = (uint8_t)(c >> 16);
+      }
       st[3 * i] = (uint16_t)(c & 0xffffu);
       st[3 * i + 1] = (uint16_t)(((c >> 16) & 0xffu) | ((px & 0xffu) << 8));
       st[3 * i + 2] = (uint16_t)((px >> 8) & 0xffffu);

@@ -346,6 +346,7 @@ class MazeEnv:
             bv.copy_(sd['body_qvel'])
         if sd.get('seed') is not None:
             self._seed = int(sd['seed'])
+            _lib.check(self._L.ogbx_maze_set_seed(self._h, self._seed))
         self._has_reset = True
 
     # ------------------------------------------------------------ reset/step

@@ -160,6 +160,17 @@ class PowderworldEnv:
                 _from_ptr(e.value, (n,), torch.int32, self.device),
                 _from_ptr(ep.value, (n,), torch.int32, self.device))
 
+    def _scalar_view(self, which):
+        """One of ctrl / elapsed / episode, int32 / uint32 [N], without asking
+        for the world pointer (handing that out marks the render cache stale,
+        ogbx_powder_state)."""
+        torch = _torch()
+        ptrs = [None, None, None, None]
+        k = {'ctrl': 1, 'elapsed': 2, 'episode': 3}[which]
+        ptrs[k] = _lib.c_void_p()
+        _lib.check(self._L.ogbx_powder_state(self._h, *ptrs))
+        return _from_ptr(ptrs[k].value, (self.num_envs,), torch.int32, self.device)
+
     def _full_views(self):
         torch = _torch()
         m, v, g = (_lib.c_void_p() for _ in range(3))
@@ -202,7 +213,7 @@ class PowderworldEnv:
 
     @property
     def cur_task_ids(self):
-        return (self._state_views()[1] >> 16) & 255
+        return (self._scalar_view('ctrl') >> 16) & 255
 
     def state_dict(self):
         w, c, e, ep = self._state_views()
@@ -221,6 +232,7 @@ class PowderworldEnv:
             ep.copy_(sd['episode'])
         if sd.get('seed') is not None:
             self._seed = int(sd['seed'])
+            _lib.check(self._L.ogbx_powder_set_seed(self._h, self._seed))
         if self._full:
             m, v, g = self._full_views()
             m.copy_(sd['momentum'])
@@ -288,7 +300,7 @@ class PowderworldEnv:
         if seed is not None:
             # gymnasium reseeding: the Philox stream of every reset env restarts
             self._seed = int(seed) & ((1 << 64) - 1)
-            _zero_episodes(self._state_views()[3], mask, self.device)
+            _zero_episodes(self._scalar_view('episode'), mask, self.device)
         elif self._seed is None:
             self._seed = (int(self._init_seed) if self._init_seed is not None
                           else int(np.random.randint(0, 2**63 - 1)))

@@ -398,3 +398,24 @@ def test_results_do_not_depend_on_wavefront_composition(gpu):
     assert np.array_equal(outp.cpu().numpy(), out.cpu().numpy()[perm])
     assert np.array_equal(contactp.cpu().numpy(), contact.cpu().numpy()[perm])
     assert contact.cpu().numpy().mean() > 0.2
+
+
+def test_state_restore_into_other_handle_carries_seed(gpu):
+    """load_state_dict into a handle reset with another seed: the restored
+    handle keys its auto-reset draws with the saved seed (ogbx_maze_set_seed),
+    so both continue identically through several auto-resets."""
+    n, K = 256, 40
+    a = _env(gpu, n, max_episode_steps=7, auto_reset=True)
+    b = _env(gpu, n, max_episode_steps=7, auto_reset=True)
+    a.reset(seed=3)
+    b.reset(seed=77)
+    g = torch.Generator().manual_seed(2)
+    acts = (torch.rand(K, n, 2, generator=g) * 2 - 1).to(gpu)
+    for t in range(3):
+        a.step(acts[t])
+    b.load_state_dict(a.state_dict())
+    for t in range(3, K):
+        oa, ra, _, tra, _ = a.step(acts[t])
+        ob, rb, _, trb, _ = b.step(acts[t])
+        assert torch.equal(oa, ob) and torch.equal(tra, trb), t
+    assert torch.equal(a.cur_goal_xy, b.cur_goal_xy)

@@ -290,3 +290,33 @@ def test_mixed_stages_single_steps_match_fused(gpu, ne, size):
     sa, sb = a.state_dict(), b.state_dict()
     for k in ('world', 'ctrl', 'elapsed', 'episode', 'momentum', 'velocity', 'goal'):
         assert torch.equal(sa[k], sb[k]), k
+
+
+@pytest.mark.parametrize('ne,size', [(5, 64), (8, 32)])
+def test_render_cache_paths_agree(gpu, ne, size):
+    """Render-only steps take their colours from the env's render cache; a step
+    after the world / velocity pointers were handed out (world_full,
+    state_dict, load_state_dict) renders from the state and rewrites the cache.
+    Both paths, and a cache made stale by load_state_dict, give the same
+    observations bit for bit."""
+    n, K, T = 8, 30, 13
+    a, b, c = (_env(gpu, n, ne=ne, size=size, max_episode_steps=11, auto_reset=True) for _ in range(3))
+    opts = dict(task_id=torch.arange(n, device=gpu) % 5 + 1)
+    a.reset(seed=2, options=opts)
+    b.reset(seed=2, options=opts)
+    c.reset(seed=99, options=dict(task_id=1))
+    rng = np.random.RandomState(5)
+    acts = rng.randint(0, max(ne, a._xy_action_size) + 1, size=(K, n))
+    for t in range(K):
+        oa, ra, *_ = a.step(acts[t])  # cache path on render-only steps
+        b.world_full()  # b renders every step from the state
+        ob, rb, *_ = b.step(acts[t])
+        assert torch.equal(oa, ob) and torch.equal(ra, rb), t
+        if t > T:
+            oc, *_ = c.step(acts[t])
+            assert torch.equal(oa, oc), t
+        if t == T:
+            assert bool(((a._scalar_view("ctrl") & 3) != 2).any())  # the next step has render-only envs
+            c.load_state_dict(a.state_dict())  # c's cache still holds its own worlds' colours
+    for k in ('world', 'momentum', 'velocity'):
+        assert torch.equal(a.state_dict()[k], c.state_dict()[k]), k
