@@ -22,16 +22,30 @@ def snap():
     torch.cuda.synchronize()
     L.ogbx_diag_pwf_rules(buf)
     return np.frombuffer(buf, dtype=np.uint64).reshape(4096, 16).astype(np.int64).copy()
+names = ['presence+rands', 'stone', 'gravity', 'sand', 'fluid', 'ice', 'water', 'fire', 'plant', 'velocity']
+
+
+def report(tag, d):
+    fw = d[:, 15].sum()
+    tot = d[:, :10].sum()
+    print(f'{level} {tag}: {fw} forwards; cycles per forward (mean over envs): {tot / fw:.0f}')
+    for k, nm in enumerate(names):
+        print(f'  {nm:15s} {d[:, k].sum() / fw:8.0f} cyc  {100 * d[:, k].sum() / tot:5.1f} %')
+
+
 for i in range(120):
     env.step(acts[i % ring])
 a = snap()
 for i in range(120, 420):
     env.step(acts[i % ring])
 b = snap()
-d = b - a
-fw = d[:, 15].sum()
-names = ['presence+rands', 'stone', 'gravity', 'sand', 'fluid', 'ice', 'water', 'fire', 'plant', 'velocity']
-tot = d[:, :10].sum()
-print(f'{level}: {fw} forwards in 300 steps; cycles per forward (mean over envs): {tot / fw:.0f}')
-for k, nm in enumerate(names):
-    print(f'  {nm:15s} {d[:, k].sum() / fw:8.0f} cyc  {100 * d[:, k].sum() / tot:5.1f} %')
+report('steady state, 300 steps', b - a)
+# the synchronized auto-reset: every env truncates at step 500 (a render-only
+# step), whose launch then replays the task's goal sequence, one forward per
+# goal action, and the reset's own forward
+for i in range(420, 499):
+    env.step(acts[i % ring])
+a = snap()
+env.step(acts[499 % ring])
+b = snap()
+report('synchronized reset step', b - a)
