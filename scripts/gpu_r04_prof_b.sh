@@ -17,5 +17,6 @@ for wl in ${WLS:-gcsample hgcsample antmaze powder powder-medium powder-hard}; d
   timeout -k 10 300 python3 bench.py --workload $wl --no-cpu-baseline > gpurun_out/bench_$wl.log 2>&1 || exit 8
   grep '^{' gpurun_out/bench_$wl.log | cut -c1-200
 done
+[ "${1:-}" = --no-default ] && exit 0
 timeout -k 10 400 python bench.py > gpurun_out/bench_default.log 2>&1 || { tail -20 gpurun_out/bench_default.log; exit 9; }
 grep '^{' gpurun_out/bench_default.log
