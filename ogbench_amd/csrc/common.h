@@ -51,36 +51,43 @@ __host__ __device__ inline uint32_t mulhi32(uint32_t a, uint32_t b) {
   return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
 }
 
-#ifdef __HIP_DEVICE_COMPILE__
-// Both halves of a round's 32x32 -> 64 product from one v_mad_u64_u32 (LLVM
-// emits a v_mul_hi_u32 + v_mul_lo_u32 pair): Philox4x32-10 throughput +6 %
-// (scripts/micro/philox_mul.hip, identical words), powder-medium step
-// -1.5 %.
-__device__ __forceinline__ void mul64(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
-  uint64_t r, c;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(c) : "v"(a), "v"(b));
-  hi = (uint32_t)(r >> 32), lo = (uint32_t)r;
-}
-#endif
-
 __host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
   const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-#ifdef __HIP_DEVICE_COMPILE__
-    uint32_t hi0, lo0, hi1, lo1;
-    mul64(M0, c.x, hi0, lo0);
-    mul64(M1, c.z, hi1, lo1);
-#else
     uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
     uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
-#endif
     u32x4 n;
     n.x = hi1 ^ c.y ^ k0;
     n.y = lo1;
     n.z = hi0 ^ c.w ^ k1;
     n.w = lo0;
+    c = n;
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// The same Philox4x32-10 with both halves of a round's 32x32 -> 64 product
+// from one v_mad_u64_u32 (LLVM emits a v_mul_hi_u32 + v_mul_lo_u32 pair):
+// +6 % throughput with identical words (scripts/micro/philox_mul.hip).  For
+// throughput-bound callers (every lane drawing, e.g. powder rand fields);
+// latency-bound chains keep the pair, whose halves issue independently.
+__device__ __forceinline__ u32x4 philox4x32_10_wide(u32x4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+  const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0, p1, c0, c1;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p0), "=s"(c0) : "v"(M0), "v"(c.x));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p1), "=s"(c1) : "v"(M1), "v"(c.z));
+    u32x4 n;
+    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    n.y = (uint32_t)p1;
+    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    n.w = (uint32_t)p0;
     c = n;
     k0 += W0;
     k1 += W1;

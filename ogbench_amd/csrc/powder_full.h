@@ -854,7 +854,7 @@ struct FullWorld {
       uint32_t w[12];
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
-        const u32x4 x = philox4x32_10({4u * g + (uint32_t)c, (uint32_t)env, ep, slot}, k0 ^ (uint32_t)(env >> 32), k1);
+        const u32x4 x = philox4x32_10_wide({4u * g + (uint32_t)c, (uint32_t)env, ep, slot}, k0 ^ (uint32_t)(env >> 32), k1);
         w[4 * c] = x.x, w[4 * c + 1] = x.y, w[4 * c + 2] = x.z, w[4 * c + 3] = x.w;
       }
 #pragma unroll

@@ -1,7 +1,7 @@
 // Microbenchmark (not shipped): Philox4x32-10 throughput on gfx950 with the
 // round's two 32x32->64 products as v_mul_hi_u32 + v_mul_lo_u32 pairs (what
 // LLVM emits for the plain C++ products) vs one v_mad_u64_u32 each (what
-// common.h's philox4x32_10 now issues).  Measured: 550 vs 583 G calls/s.
+// common.h's philox4x32_10_wide issues).  Measured: 550 vs 583 G calls/s.
 // Build: hipcc -O3 --offload-arch=gfx950 scripts/micro/philox_mul.hip -o _abx/philox_mul
 #include <hip/hip_runtime.h>
 #include <cstdio>
