@@ -52,7 +52,7 @@ struct alignas(16) PwFullShared {
   uint32_t lut[32];
   int32_t elem_ids[8];
   float vel_q[8];  // angle-bin thresholds on q (PowderParams::vel_q)
-  int32_t red[16];    // presence()
+  alignas(8) int32_t red[16];  // presence(); fire() reads it as 8 x uint64 (hot rows per wave)
   int32_t red_e[16];  // errors()
   int32_t red_v[16];  // block_or()
   // per-row cell bitmasks (bit c = column c) of rule predicates, rows -1..H:
@@ -331,15 +331,42 @@ struct FullWorld {
     commit_moved(mv, [&](int i) { s.a[i] = (uint8_t)rd(s.a[i]); });
   }
 
+  // rows (bit r) holding a cell of the id set `ids`: W = 64 (a wave is a row),
+  // one 64-bit word per wave through s.red; ~0 at W = 32.  Contains a barrier.
+  __device__ __forceinline__ uint64_t rows_with(uint32_t ids) const {
+    if constexpr (W == 64) {
+      uint64_t mine = 0;
+#pragma unroll
+      for (int k = 0; k < CPT; ++k)
+        mine |= (__ballot(in_set(ids, fid(s.a[cell(k)]))) != 0ull ? 1ull : 0ull) << row(k);
+      if ((threadIdx.x & 63) == 0) reinterpret_cast<uint64_t*>(s.red)[threadIdx.x >> 6] = mine;
+      sync();
+      uint64_t all = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) all |= reinterpret_cast<const uint64_t*>(s.red)[w];
+      return all;
+    } else {
+      return ~0ull;
+    }
+  }
+  __device__ static __forceinline__ uint64_t rotl1(uint64_t x) { return (x << 1) | (x >> 63); }
+
   __device__ __forceinline__ void sand() const {
     fence_idx();
+    // A cell changes only if it holds sand / dust or the cell above-diagonal
+    // (periodic) does, so rows with neither in rows r, r-1 skip their cells;
+    // pass 0 moves sand / dust at most one row down, which widens the set
+    // for pass 1.
+    const uint64_t S0 = rows_with(bit(kSand) | bit(kDust)), S1 = S0 | rotl1(S0);
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       const int go = pass == 0 ? -1 : 1;        // fall toward -1 (left) then +1 (right)
       const uint32_t fl = pass == 0 ? 1u : 0u;  // fall_dir: rm > 0.5, then rm <= 0.5
+      const uint64_t act = pass == 0 ? S0 | rotl1(S0) : S1 | rotl1(S1);
       Moves mvs;
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
+        if (!((act >> row(k)) & 1ull)) continue;  // wave-uniform at W = 64
         const int i = cell(k), ibl = nb(k, 1, go), iar = nb(k, -1, -go);
         const uint32_t a = s.a[i], bl = s.a[ibl], ar = s.a[iar];
         const bool elem = in_set(bit(kSand) | bit(kDust), fid(a));
@@ -502,13 +529,37 @@ struct FullWorld {
       flb |= in_set(bit(kFire) | bit(kLava), id) ? 1u << k : 0u;
     }
     row_masks(hotm, [&](int k) { return ((flb >> k) & 1u) != 0u; });
+    // rows holding fire or lava (W = 64: a wave is a row; one 64-bit word per
+    // wave, OR-ed after the barrier).  Every effect of the rule needs fire or
+    // lava in the cell's zero-padded 3x3 (burns, ignition, fading), or a
+    // burning 4-neighbour (impulses, periodic), so a row with no hot cell in
+    // rows r-1..r+1 (A3) changes nothing and one with none in A3 of r-1..r+1
+    // (A5, periodic) reads no non-zero burn flag: such rows skip their cells.
+    uint64_t A3 = ~0ull, A5 = ~0ull;
+    if constexpr (W == 64) {
+      uint64_t mine = 0;
+#pragma unroll
+      for (int k = 0; k < CPT; ++k) mine |= (__ballot((flb >> k) & 1u) != 0ull ? 1ull : 0ull) << row(k);
+      if ((threadIdx.x & 63) == 0) reinterpret_cast<uint64_t*>(s.red)[threadIdx.x >> 6] = mine;
+    }
     sync();
+    if constexpr (W == 64) {
+      uint64_t hot = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) hot |= reinterpret_cast<const uint64_t*>(s.red)[w];
+      A3 = hot | (hot << 1) | (hot >> 1);
+      A5 = A3 | (A3 << 1) | (A3 >> 63) | (A3 >> 1) | (A3 << 63);
+    }
     // burn decisions; f2 bit 0: burns (pushes its 4 neighbours with 8), bit 1:
     // dust near fire (pushes with 30)
     Codes conv = 0;  // 8 bits per cell: new id + 1, 0 = unchanged
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
+      if (!((A3 >> row(k)) & 1ull)) {  // wave-uniform at W = 64
+        s.f2[i] = 0;
+        continue;
+      }
       const uint32_t id = fid(s.a[i]);
       const bool nr = any3x3(hotm, k);
       const bool p005 = ri_lt(k, kRi005), p02 = ri_lt(k, kRi02);
@@ -532,6 +583,7 @@ struct FullWorld {
     // below, right; then the conversions (own cells, in place)
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
+      if (!((A5 >> row(k)) & 1ull)) continue;
       const int i = cell(k);
       const uint32_t L = s.f2[nb(k, 0, -1)], U = s.f2[nb(k, -1, 0)], D = s.f2[nb(k, 1, 0)], R = s.f2[nb(k, 0, 1)];
       const uint32_t to = (uint32_t)(conv >> (8 * k)) & 0xFFu;
@@ -556,6 +608,7 @@ struct FullWorld {
     uint32_t fade = 0, nbr = 0;  // bit k: some burnable cell in the 3x3
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
+      if (!((A3 >> row(k)) & 1ull)) continue;  // no fire / lava cell, no source
       const uint32_t id = fid(s.a[cell(k)]);
       const bool b = any3x3(burnm, k);
       nbr |= b ? 1u << k : 0u;
@@ -571,6 +624,7 @@ struct FullWorld {
     Codes conv2 = 0;
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
+      if (!((A3 >> row(k)) & 1ull)) continue;  // no source in the 3x3, no fading fire
       const uint32_t id = fid(s.a[cell(k)]);
       const bool burn_empty = (id == kEmpty) & ri_lt(k, kRi03) & any3x3(srcm, k);
       bool fd = (fade >> k) & 1u;

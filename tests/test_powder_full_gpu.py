@@ -85,6 +85,45 @@ def test_forward_matches_oracle_seeded(gpu, ne, size):
     assert np.array_equal(got, ref), _diff(got, ref)
 
 
+@pytest.mark.parametrize('walls', [True, False])
+def test_forward_sparse_rows_matches_oracle(gpu, walls):
+    """64x64 worlds where fire / lava sit in a few rows only, so the fire
+    rule's per-row skipping (rows with no hot cell within one row, and rows
+    with no burn flag within one row, periodic) is exercised next to the rows
+    it runs on; without border walls, hot cells at rows 0 / 63 reach across
+    the periodic boundary (impulses use np.roll).  Bit-exact vs the oracle."""
+    rng = np.random.RandomState(7 if walls else 8)
+    n, size, steps = 3, 64, 8
+    ids = np.zeros((n, size, size), np.int64)
+    burn = [orc.WOOD, orc.PLANT, orc.GAS, orc.DUST, orc.SAND, orc.WATER, orc.ICE, orc.STONE]
+    for e in range(n):
+        rows = rng.choice(np.arange(size), size=10, replace=False)
+        for r in rows:  # sparse rows of burnables and others
+            cols = rng.rand(size) < 0.5
+            ids[e, r, cols] = rng.choice(burn, size=int(cols.sum()))
+        hot = [1, 2, 62] if walls else [1, 31]
+        for r in hot + [int(rows[0])]:
+            cols = rng.rand(size) < 0.3
+            ids[e, r, cols] = rng.choice([orc.FIRE, orc.LAVA, orc.DUST, orc.WOOD], size=int(cols.sum()))
+        if not walls:  # dust at row 0 burns next to row 1's fire and pushes row 63 (periodic)
+            ids[e, 0, :] = orc.DUST
+            ids[e, 1, ::2] = orc.FIRE
+    if walls:
+        ids[:, 0, :] = ids[:, -1, :] = ids[:, :, 0] = ids[:, :, -1] = orc.WALL
+    w = orc.from_ids(ids)
+    w[:, 3:5] = (rng.randn(n, 2, size, size) * 2.5).astype(np.float32) * (rng.rand(n, 1, size, size) < 0.05)
+    w = w.astype(np.float32)
+    rand = rng.rand(steps, n, 3, size, size).astype(np.float32)
+    env = _env(gpu, 1, ne=8, size=size)
+    got = env.forward_full(w, steps, rand=rand).cpu().numpy()
+    ref = w
+    for t in range(steps):
+        ref = orc.forward(ref, [rand[t][:, k] for k in range(3)])
+    assert np.array_equal(got, ref), _diff(got, ref)
+    one = env.forward_full(w, 1, rand=rand[:1]).cpu().numpy()
+    assert np.array_equal(one, orc.forward(w, [rand[0][:, k] for k in range(3)]))
+
+
 def _padded_reset_rand(env, r, task):
     """[1, R, 3, H, W]: goal rows then the reset forward at row len(task)."""
     H = env._world_size
