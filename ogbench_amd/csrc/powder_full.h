@@ -648,9 +648,26 @@ struct FullWorld {
       const uint32_t x = fid(s.a[cell(k)]);
       return in_set(bit(kIce) | bit(kWood), x);
     });
+    // every conversion needs a plant in the zero-padded 3x3 (count >= 1), so
+    // rows with no plant in rows r-1..r+1 skip their cells (W = 64)
+    uint64_t act = ~0ull;
+    if constexpr (W == 64) {
+      uint64_t mine = 0;
+#pragma unroll
+      for (int k = 0; k < CPT; ++k)
+        mine |= (__ballot(fid(s.a[cell(k)]) == kPlant) != 0ull ? 1ull : 0ull) << row(k);
+      if ((threadIdx.x & 63) == 0) reinterpret_cast<uint64_t*>(s.red)[threadIdx.x >> 6] = mine;
+    }
     sync();
+    if constexpr (W == 64) {
+      uint64_t pr = 0;
+#pragma unroll
+      for (int w = 0; w < NT / 64; ++w) pr |= reinterpret_cast<const uint64_t*>(s.red)[w];
+      act = pr | (pr << 1) | (pr >> 1);
+    }
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
+      if (!((act >> row(k)) & 1ull)) continue;
       const uint32_t id = fid(s.a[cell(k)]);
       const bool grow = id == kWater && ri_lt(k, kRi005);
       const bool seed = id == kEmpty && ri_lt(k, kRi02);
