@@ -864,15 +864,30 @@ __global__ void __launch_bounds__(256) pwf_light_step_kernel(
       cb[k] = (uint8_t)(col[k] >> 16);
     }
   }
+  // the thread's CPT cells are 6 * CPT contiguous observation bytes: packed
+  // in registers (cell k at byte 6k: word 3k/2, at bit 0 or 16) and staged
+  // with 16- / 8-byte LDS writes
+  uint32_t ow[CPT * 6 / 4];
+#pragma unroll
+  for (int j = 0; j < CPT * 6 / 4; ++j) ow[j] = 0u;
 #pragma unroll
   for (int k = 0; k < CPT; ++k) {
-    const int i = c0 + k, cc = i % WS;
-    const uint32_t c = col[k];
+    const int cc = (c0 + k) % WS;
     const bool fr = stage == 1 || (stage == 2 && cc >= rx && cc < rx + brush);
-    const uint32_t px = fr ? acol : 0u;
-    st[3 * i] = (uint16_t)(c & 0xffffu);
-    st[3 * i + 1] = (uint16_t)(((c >> 16) & 0xffu) | ((px & 0xffu) << 8));
-    st[3 * i + 2] = (uint16_t)((px >> 8) & 0xffffu);
+    const uint64_t six = (uint64_t)(col[k] & 0xFFFFFFu) | ((uint64_t)((fr ? acol : 0u) & 0xFFFFFFu) << 24);
+    const int wi = (6 * k) >> 2, sh = ((6 * k) & 3) * 8;  // sh in {0, 16}
+    const uint64_t v = six << sh;
+    ow[wi] |= (uint32_t)v;
+    ow[wi + 1] |= (uint32_t)(v >> 32);
+  }
+  if constexpr (CPT == 16) {
+    uint4* dst = reinterpret_cast<uint4*>(st) + t * 6;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) dst[j] = make_uint4(ow[4 * j], ow[4 * j + 1], ow[4 * j + 2], ow[4 * j + 3]);
+  } else {
+    uint2* dst = reinterpret_cast<uint2*>(st) + t * 3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dst[j] = make_uint2(ow[2 * j], ow[2 * j + 1]);
   }
   __syncthreads();
   const uint4* src = reinterpret_cast<const uint4*>(st);
