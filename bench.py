@@ -779,7 +779,7 @@ def _powder_phases(env, step, start, dev):
     their own, rarely under random actions).  Steady state: the mean of a
     window of whole 3-step action cycles that contains no synchronized reset;
     reset step: the one step in which the synchronized reset happens."""
-    el = int(env.state_dict()['elapsed'][0])
+    el = int(env._scalar_view('elapsed')[0])  # (state_dict would mark the render cache stale)
     T = env.max_episode_steps
     left = T - el  # the step with index start + left - 1 is the synchronized reset
     i = start
@@ -808,7 +808,7 @@ def _powder_phases(env, step, start, dev):
     b.record(stream)
     torch.cuda.synchronize(dev)
     out['sync_reset_step_ms'] = a.elapsed_time(b)
-    out['sync_reset_envs'] = int((env.state_dict()['elapsed'] == 0).sum())
+    out['sync_reset_envs'] = int((env._scalar_view('elapsed') == 0).sum())
     out['sync_reset_every_steps'] = T
     return out
 
