@@ -1120,6 +1120,15 @@ struct ogbx_powder_env {
   // write through it); the next step then renders from the state and rewrites
   // the cache of every env
   bool cache_stale = true;
+  // steps since the last reset of every env (-1: unknown, e.g. after a masked
+  // reset).  Envs reset together step in phase, so the host can tell the
+  // steps on which every in-phase env needs the full kernel (its forward
+  // step, or the synchronized truncation + auto-reset) and not launch
+  // pwf_light_step_kernel, whose every workgroup would exit.  A wrong guess
+  // is harmless: pwf_step_kernel without the skip list steps render-only
+  // envs itself, bit-identically (only slower), so out-of-phase envs (an
+  // earlier success + auto-reset, a restored state) stay correct.
+  int64_t phase = -1;
   uint64_t seed = 0;
   bool was_reset = false;
 };
@@ -1329,6 +1338,7 @@ ogbx_status ogbx_powder_reset(ogbx_powder_t e, const int32_t* task_id, const uin
     OGBX_LAUNCHED("pw_reset_kernel");
   }
   e->was_reset = true;
+  e->phase = mask == nullptr ? 0 : -1;
   return OGBX_OK;
 }
 
@@ -1347,7 +1357,13 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
   seed_key(e->seed, kTagPowderAction, &a0, &a1);
   seed_key(e->seed, kTagPowderRand, &r0, &r1);
   if (e->full) {
-    const bool light = e->light && k_steps == 1;
+    bool all_full = false;  // every in-phase env runs the full kernel this step
+    if (e->phase >= 0 && k_steps == 1) {
+      const int64_t T = e->P.max_steps > 0 ? e->P.max_steps : 0;
+      const int64_t j = (auto_reset && T > 0) ? e->phase % T : e->phase;  // the env's elapsed steps
+      all_full = j % 3 == 2 || (auto_reset && T > 0 && j + 1 >= T);
+    }
+    const bool light = e->light && k_steps == 1 && !all_full;
     if (light) {
       PW_LAUNCH(pwf_light_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, action, draws, obs, reward,
                 terminated, truncated, success, auto_reset, a0, a1, e->handled, (int32_t)e->cache_stale);
@@ -1358,6 +1374,7 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
               light ? e->handled : (const uint8_t*)nullptr, (int32_t)e->cache_stale);
     OGBX_LAUNCHED("pwf_step_kernel");
     e->cache_stale = false;  // every env's cache was written by one of the two kernels
+    if (e->phase >= 0) e->phase += k_steps;
   } else {
     PW_LAUNCH(pw_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, e->goals, e->n, action, draws, k_steps, obs,
               reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1);
