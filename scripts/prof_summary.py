@@ -59,20 +59,26 @@ def main():
     shutil.copyfile(stats, dst)
     with open(stats) as f:
         rows = list(csv.DictReader(f))
-    # '+'-joined kernels (a step made of several launches, one each per step):
-    # per-step duration and bytes are the sums over the parts
+    # '+'-joined kernels (a step made of several launches): per-step duration
+    # and bytes are the sums over the parts, each part weighted by its share of
+    # the steps (a part may skip steps: the powder light kernel is not launched
+    # on steps where every env runs the full kernel); steps = the most calls
     parts = a.kernel.split('+')
-    avg_ns, calls, fetch, write, nf, nw = 0.0, None, 0.0, 0.0, None, None
+    per = []
     for k in parts:
+        avg, n = 0.0, 0
         for row in rows:
             if k in row['Name']:
-                avg_ns += float(row['AverageNs'])
-                calls = int(row['Calls']) if calls is None else min(calls, int(row['Calls']))
+                avg, n = float(row['AverageNs']), int(row['Calls'])
         fk, nfk = counter_avg(os.path.join(a.out, f'pmc_fetch_{a.workload}'), 'FETCH_SIZE', k)
         wk, nwk = counter_avg(os.path.join(a.out, f'pmc_write_{a.workload}'), 'WRITE_SIZE', k)
-        fetch, write = fetch + fk, write + wk
-        nf = nfk if nf is None else min(nf, nfk)
-        nw = nwk if nw is None else min(nw, nwk)
+        per.append((avg, n, fk, nfk, wk, nwk))
+    calls = max(p[1] for p in per)
+    nf = max(p[3] for p in per)
+    nw = max(p[5] for p in per)
+    avg_ns = sum(p[0] * p[1] for p in per) / calls
+    fetch = sum(p[2] * p[3] for p in per) / nf
+    write = sum(p[4] * p[5] for p in per) / nw
     rec = dict(
         workload=a.workload,
         round=a.round,
