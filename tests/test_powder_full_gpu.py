@@ -359,3 +359,39 @@ def test_render_cache_paths_agree(gpu, ne, size):
             c.load_state_dict(a.state_dict())  # c's cache still holds its own worlds' colours
     for k in ('world', 'momentum', 'velocity'):
         assert torch.equal(a.state_dict()[k], c.state_dict()[k]), k
+
+
+@pytest.mark.parametrize('ne,size', [(5, 64), (8, 32)])
+def test_out_of_phase_envs_after_full_reset_match_fused(gpu, ne, size):
+    """The host skips the light kernel on steps where every env reset together
+    needs the full kernel (ogbx_powder_env::phase).  Envs out of that phase
+    (here: a mixed-stage state loaded after an all-env reset, so the host's
+    guess is wrong for some envs on every step) must still step bit-for-bit as
+    the fused rollout from the same state."""
+    n, K = 9, 16
+    src = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    src.reset(seed=4, options=dict(task_id=torch.arange(n, device=gpu) % 5 + 1))
+    rng = np.random.RandomState(12)
+    hi = max(ne, src._xy_action_size) + 1
+    src.step(rng.randint(0, hi, size=n))
+    src.reset(options=dict(task_id=2), mask=torch.tensor([i % 3 == 1 for i in range(n)], dtype=torch.uint8,
+                                                           device=gpu))
+    src.step(rng.randint(0, hi, size=n))
+    sd = src.state_dict()
+    assert len(set((sd['ctrl'] & 3).tolist())) >= 2
+    a = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    b = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    a.reset(seed=4, options=dict(task_id=1))  # all-env reset: phase 0 on the host
+    a.load_state_dict(sd)                       # ... but the envs are not in that phase
+    b.reset(seed=4, options=dict(task_id=1))
+    b.load_state_dict(sd)
+    acts = rng.randint(0, hi, size=(K, n))
+    out = b.rollout(acts)
+    for t in range(K):
+        ob, rew, term, trunc, info = a.step(acts[t])
+        assert torch.equal(out['obs'][t], ob), t
+        assert torch.equal(out['reward'][t], rew), t
+        assert torch.equal(out['truncated'][t].bool(), trunc), t
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in ('world', 'ctrl', 'elapsed', 'episode', 'momentum', 'velocity', 'goal'):
+        assert torch.equal(sa[k], sb[k]), k
