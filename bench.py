@@ -6,8 +6,8 @@ pointmaze-large (pointmaze-large-navigate-v0), 1/2/4/8 MI355X.
 A step = one ``env.step(action)`` of all envs of this rank: one launch of
 ``maze_step_kernel`` through the C-ABI (Python -> ctypes -> libogbx), with the
 [N,2] float32 actions already resident in HBM (pre-generated ring, seed 1) and
-same-step auto-reset.  Timed region: barrier + synchronize, K steps, barrier +
-synchronize; the max over ranks is reported.
+same-step auto-reset.  Timed region: barrier + synchronize, K steps,
+synchronize (clock read), barrier; the max over ranks is reported.
 
 Multi-GPU (the metric: N = 65,536 envs in total on 1/2/4/8 GPUs): one process
 per GPU; env i lives on rank i // (N/G) (``ogbench_amd.sharding``), each rank's
@@ -77,7 +77,13 @@ def _max_over_ranks(x, world, dev):
 def _timed(fn, steps, world, dev, span=None):
     """Wall time of `steps` calls between barrier + synchronize on both sides,
     max over ranks.  span (a list): receives the device time of the same
-    region from a HIP event pair on the launch stream, in ms."""
+    region from a HIP event pair on the launch stream, in ms.
+
+    Each rank's clock runs from the end of the leading barrier + synchronize
+    to the end of its own trailing synchronize; the trailing barrier follows
+    the clock read, so the job time (max over ranks) covers every rank's K
+    steps but not the barrier's own collective latency (tens of us over
+    RCCL, comparable to 20 steps of a 12-us launch)."""
     _barrier(world)
     torch.cuda.synchronize(dev)
     if span is not None:
@@ -89,8 +95,8 @@ def _timed(fn, steps, world, dev, span=None):
     if span is not None:
         b.record(torch.cuda.current_stream(dev))
     torch.cuda.synchronize(dev)
-    _barrier(world)
     dt = time.perf_counter() - t0
+    _barrier(world)
     if span is not None:
         span.append(a.elapsed_time(b))
     return _max_over_ranks(dt, world, dev)

@@ -32,7 +32,11 @@
 extern "C" {
 #endif
 
-#define OGBX_ABI_VERSION 4
+/* History: 4 = rounds 1-3; 5 adds ogbx_gc_sample_ahead, ogbx_hgc_sample_ahead,
+ * ogbx_maze_set_seed, ogbx_powder_set_seed, ogbx_stream_version,
+ * ogbx_powder_state_view and ogbx_powder_state_written (no entry point of 4
+ * changed its signature or meaning). */
+#define OGBX_ABI_VERSION 5
 
 typedef enum {
   OGBX_OK = 0,
@@ -398,8 +402,10 @@ ogbx_status ogbx_gc_sample(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
  * ahead_out (NULL: not computed), so a call's draw chain (Philox -> picks ->
  * goals) is off its own critical path.  ahead_in / ahead_out are caller-owned
  * device buffers of OGBX_GC_AHEAD_WORDS 8-byte words per sample, ordered on
- * `stream`; ahead_in must hold what the previous launch stored for exactly
- * this (seed, call_index, batch, num_batches, buffer, config).  Every output
+ * `stream` (a launch on another stream needs a pair of its own: it would
+ * overwrite selectors an in-flight launch still reads); ahead_in must hold
+ * what the previous launch stored for exactly this (seed, call_index,
+ * batch, num_batches, buffer, config), i.e. for call_index - 1's successor.  Every output
  * is bit-identical to ogbx_gc_sample's with the same seed and call_index.
  * Same reference as ogbx_gc_sample (datasets.py:213-327). */
 #define OGBX_GC_AHEAD_WORDS 8
@@ -566,9 +572,25 @@ ogbx_status ogbx_powder_step(ogbx_powder_t env, const int32_t* action, int32_t k
  * ogbx_maze_state).  Any argument may be NULL.  Writable (state restore):
  * medium/hard envs keep a render cache of the world's colours, and asking for
  * `world` marks it stale, so the next ogbx_powder_step renders from the state
- * (write through the pointer before that step, not after it). */
+ * (a write through a kept pointer after that step must be announced with
+ * ogbx_powder_state_written; readers use ogbx_powder_state_view). */
 ogbx_status ogbx_powder_state(ogbx_powder_t env, uint8_t** world, int32_t** ctrl,
                               int32_t** elapsed, uint32_t** episode);
+
+/* Read-only views of the state (world as ogbx_powder_state; momentum,
+ * velocity and goal ids as ogbx_powder_full_state, medium/hard only).  Unlike
+ * those two, this hands out no writable pointer, so the render cache and the
+ * phase guess stay valid: the accessor for readers that run every step
+ * (PowderworldEnv.world_ids / world_full).  Any argument may be NULL. */
+ogbx_status ogbx_powder_state_view(ogbx_powder_t env, const uint8_t** world, const int8_t** momentum,
+                                   const float** velocity, const uint8_t** goal_ids);
+
+/* The caller wrote the state through a pointer of ogbx_powder_state /
+ * ogbx_powder_full_state (a restore, an edit): marks the render cache stale,
+ * forgets the phase guess and allows stepping without a reset.  Needed when
+ * the write comes after a step that followed the pointer's hand-out (a host
+ * that keeps the pointers); harmless otherwise. */
+ogbx_status ogbx_powder_state_written(ogbx_powder_t env);
 
 /* The seed of the steps' Philox draws (invalid-action replacements, rand
  * fields, auto-resets), as the last ogbx_powder_reset set it; restores it with

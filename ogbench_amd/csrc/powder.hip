@@ -1395,6 +1395,26 @@ ogbx_status ogbx_powder_state(ogbx_powder_t e, uint8_t** world, int32_t** ctrl, 
   return OGBX_OK;
 }
 
+ogbx_status ogbx_powder_state_view(ogbx_powder_t e, const uint8_t** world, const int8_t** momentum,
+                                   const float** velocity, const uint8_t** goal_ids) {
+  OGBX_CHECK(e, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->full || (!momentum && !velocity && !goal_ids), OGBX_EINVAL,
+             "easy worlds carry no momentum / velocity / per-env goals");
+  if (world) *world = e->S.world;
+  if (momentum) *momentum = e->S.mom;
+  if (velocity) *velocity = reinterpret_cast<const float*>(e->S.vel);
+  if (goal_ids) *goal_ids = e->S.goal_env;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_powder_state_written(ogbx_powder_t e) {
+  OGBX_CHECK(e, OGBX_EINVAL, "null handle");
+  e->cache_stale = true;
+  e->phase = -1;  // a restored state need not step in phase with the last reset
+  e->was_reset = true;
+  return OGBX_OK;
+}
+
 ogbx_status ogbx_powder_set_seed(ogbx_powder_t e, uint64_t seed) {
   OGBX_CHECK(e, OGBX_EINVAL, "null handle");
   e->seed = seed;

@@ -164,6 +164,12 @@ def nonzero_positive(x):
     return out[: int(cnt.item())]
 
 
+def _skey(stream):
+    """A stream handle as a hashable, comparable key (ctypes.c_void_p
+    objects compare by identity, so two handles of one stream never match)."""
+    return stream.value if isinstance(stream, ctypes.c_void_p) else stream
+
+
 def _to_device(v, device):
     torch = _torch()
     if isinstance(v, torch.Tensor):
@@ -313,6 +319,7 @@ class GCDataset:
         self._lookahead = bool(config.get('lookahead', self._LOOKAHEAD_DEFAULT))
         self._ahead_bufs = None
         self._ahead = None
+        self.ahead_hits = 0  # calls whose selectors the previous launch stored (diagnostic)
 
     # ---------------------------------------------------------------- helpers
     _RECORD_MAX = 128  # one L2 line
@@ -437,20 +444,38 @@ class GCDataset:
     _AHEAD_WORDS = 8   # OGBX_GC_AHEAD_WORDS
     _HGC_AHEAD_WORDS = 20  # OGBX_HGC_AHEAD_WORDS
 
+    _AHEAD_STREAMS = 8  # streams with a buffer pair of their own before the pairs are recycled
+
     def _ahead_slots(self, B, nb, stream, call, words):
         """(ahead_in, ahead_out, index of ahead_out) for call `call`: the
         selectors stored by the previous launch when it stored them for exactly
-        this (batch, num_batches, stream, call), else none (computed in line)."""
-        if self._ahead_bufs is None or self._ahead_bufs[0].numel() < self._AHEAD_MAX * words:
+        this (batch, num_batches, stream, call), else none (computed in line).
+
+        Every stream has its own ping-pong pair, allocated on (and so only
+        ever reused in the order of) that stream: a launch on another stream
+        never writes a buffer a launch still in flight on this one reads or
+        writes."""
+        key = _skey(stream)
+        if self._ahead_bufs is None:
+            self._ahead_bufs = {}
+        pair = self._ahead_bufs.get(key)
+        if pair is None or pair[0][0].numel() < self._AHEAD_MAX * words:
             torch = _torch()
-            self._ahead_bufs = [torch.empty(self._AHEAD_MAX * words, dtype=torch.int64, device=self.device)
-                                for _ in range(2)]
-            self._ahead_ptrs = [t.data_ptr() for t in self._ahead_bufs]
-            self._ahead = None
+            if len(self._ahead_bufs) >= self._AHEAD_STREAMS:
+                # the caching allocator hands a freed block out again only in
+                # its stream's order, so dropping a pair is stream-safe
+                self._ahead_bufs.clear()
+                self._ahead = None
+            bufs = [torch.empty(self._AHEAD_MAX * words, dtype=torch.int64, device=self.device) for _ in range(2)]
+            pair = self._ahead_bufs[key] = (bufs, [t.data_ptr() for t in bufs])
+            if self._ahead is not None and self._ahead[0][2] == key:
+                self._ahead = None
+        ptrs = pair[1]
         a = self._ahead
-        if a is not None and a[0] == (B, nb, stream, call):
-            return self._ahead_ptrs[a[1]], self._ahead_ptrs[1 - a[1]], 1 - a[1]
-        return None, self._ahead_ptrs[0], 0
+        if a is not None and a[0] == (B, nb, key, call):
+            self.ahead_hits += 1
+            return ptrs[a[1]], ptrs[1 - a[1]], 1 - a[1]
+        return None, ptrs[0], 0
 
     def _launch_plain(self, col_p, ncols, B, nb, seed, call, idx_p, vg_p, ag_p, masks_p, rewards_p, stream):
         """One Philox-mode GCDataset.sample launch.  Small calls (<= 1024
@@ -466,7 +491,7 @@ class GCDataset:
         src, dst, which = self._ahead_slots(B, nb, stream, call, self._AHEAD_WORDS)
         st = self._L.ogbx_gc_sample_ahead(self._buf, self._cfg, col_p, ncols, B, nb, seed, call, src, dst, idx_p,
                                           vg_p, ag_p, masks_p, rewards_p, stream)
-        self._ahead = ((B, nb, stream, call + 1), which) if st == 0 else None
+        self._ahead = ((B, nb, _skey(stream), call + 1), which) if st == 0 else None
         return st
 
     def sample(self, batch_size, idxs=None, evaluation=False, draws=None, record_draws=False,
@@ -763,7 +788,7 @@ class HGCDataset(GCDataset):
             src, dst, which = self._ahead_slots(B, nb, stream, call, self._HGC_AHEAD_WORDS)
             st = self._Lh.ogbx_hgc_sample_ahead(self._buf, self._cfg, self._hcfg, col_arr, ncols, B, nb, seed, call,
                                                 src, dst, outs, stream)
-            self._ahead = ((B, nb, stream, call + 1), which) if st == 0 else None
+            self._ahead = ((B, nb, _skey(stream), call + 1), which) if st == 0 else None
         else:
             self._ahead = None
             st = self._Lh.ogbx_hgc_sample(self._buf, self._cfg, self._hcfg, col_arr, ncols, B, nb, dr, seed, call,

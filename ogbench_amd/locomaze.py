@@ -536,13 +536,16 @@ class MazeEnv:
             assert rs.shape == (self.num_envs, 29)
             rs = rs.data_ptr()
         hit = self._wrap_cache.get((id(qpos), id(qvel)))
-        # a hit is re-checked against the storage pointer and strides it was
-        # validated with (set_ / .data = / a reallocating resize_ move the
-        # pointer; transpose_ and a reshaping resize_ change the strides);
+        # a hit is re-checked against the storage pointer, strides and row
+        # count it was validated with (set_ / .data = / a reallocating resize_
+        # move the pointer; transpose_ and a reshaping resize_ change the
+        # strides; an in-place shrinking resize_ keeps both but not the rows);
         # anything else revalidates.  (~0.2 us per tensor call; the launch is
         # ~5 us)
+        n = self.num_envs
         if (hit is not None and hit[0] is qpos and hit[1] is qvel and qpos.data_ptr() == hit[2]
-                and qvel.data_ptr() == hit[3] and qpos.stride() == (15, 1) and qvel.stride() == (14, 1)):
+                and qvel.data_ptr() == hit[3] and qpos.stride() == (15, 1) and qvel.stride() == (14, 1)
+                and qpos.shape[0] == n and qvel.shape[0] == n):
             qp, vp = hit[2], hit[3]
         else:
             qp, vp = self._wrap_validate(qpos, qvel)

@@ -171,6 +171,23 @@ class PowderworldEnv:
         _lib.check(self._L.ogbx_powder_state(self._h, *ptrs))
         return _from_ptr(ptrs[k].value, (self.num_envs,), torch.int32, self.device)
 
+    def _read_views(self):
+        """Read-only (world, momentum, velocity, goal ids) views through
+        ogbx_powder_state_view: no writable pointer is handed out, so the
+        render cache stays valid (momentum/velocity/goal None for easy)."""
+        torch = _torch()
+        ptrs = [_lib.c_void_p() for _ in range(4)]
+        if not self._full:
+            ptrs[1:] = [None, None, None]
+        _lib.check(self._L.ogbx_powder_state_view(self._h, *ptrs))
+        n, H = self.num_envs, self._world_size
+        w = _from_ptr(ptrs[0].value, (n, H, H), torch.uint8, self.device)
+        if not self._full:
+            return w, None, None, None
+        return (w, _from_ptr(ptrs[1].value, (n, H, H), torch.int8, self.device),
+                _from_ptr(ptrs[2].value, (n, H, H, 2), torch.float32, self.device),
+                _from_ptr(ptrs[3].value, (n, H, H), torch.uint8, self.device))
+
     def _full_views(self):
         torch = _torch()
         m, v, g = (_lib.c_void_p() for _ in range(3))
@@ -183,7 +200,7 @@ class PowderworldEnv:
     def goal_ids(self):
         """Goal element ids per env, uint8 [N, H, W] (reference cur_goal_world)."""
         if self._full:
-            return self._full_views()[2]
+            return self._read_views()[3]
         torch = _torch()
         g = torch.as_tensor(self.goal_worlds(), device=self.device)
         return g[(self.cur_task_ids.long() - 1).clamp(min=0)]
@@ -191,7 +208,7 @@ class PowderworldEnv:
     def world_full(self):
         """Worlds in the reference's (N, 9, H, W) float32 layout."""
         torch = _torch()
-        w = self._state_views()[0]
+        w, m, v, _ = self._read_views()
         ids = (w & 31).long()
         dens = torch.tensor([1, 4, 3, 2, 0, 4, 4, 0, 4, 3, 3, 2, 2, 4, 2, 4, 3, 3, 3, 4, 3, 0, 0, 0, 0, 0, 0, 0, 0,
                              0, 0, 0], dtype=torch.float32, device=self.device)
@@ -201,7 +218,6 @@ class PowderworldEnv:
         out[:, 2] = ((w >> 5) & 1).float()
         out[:, 8] = ((w >> 6) & 1).float()
         if self._full:
-            m, v, _ = self._full_views()
             out[:, 3] = v[..., 0]
             out[:, 4] = v[..., 1]
             out[:, 6] = m.float()
@@ -209,17 +225,17 @@ class PowderworldEnv:
 
     def world_ids(self):
         """Element id of every cell, uint8 [N, H, W] (reference self._world[:, 0])."""
-        return self._state_views()[0] & 31
+        return self._read_views()[0] & 31
 
     @property
     def cur_task_ids(self):
         return (self._scalar_view('ctrl') >> 16) & 255
 
     def state_dict(self):
-        w, c, e, ep = self._state_views()
+        w, m, v, g = self._read_views()
+        c, e, ep = (self._scalar_view(k) for k in ('ctrl', 'elapsed', 'episode'))
         sd = dict(world=w.clone(), ctrl=c.clone(), elapsed=e.clone(), episode=ep.clone(), seed=self._seed)
         if self._full:
-            m, v, g = self._full_views()
             sd.update(momentum=m.clone(), velocity=v.clone(), goal=g.clone())
         return sd
 
@@ -238,6 +254,7 @@ class PowderworldEnv:
             m.copy_(sd['momentum'])
             v.copy_(sd['velocity'])
             g.copy_(sd['goal'])
+        _lib.check(self._L.ogbx_powder_state_written(self._h))
 
     def forward(self, worlds, steps=1):
         """PWSim.forward (sim.py:363-380) on packed worlds uint8 [n, H, W]."""

@@ -2,6 +2,7 @@
 # Build _abx/libogbx_<name>.so: libogbx with $SRC.hip (default locomaze) compiled under
 # extra flags (the other objects from build/obj, built by `make`).  Run here.
 # usage: scripts/build_maze_variant.sh <name> [-DFLAG ...]
+# (-D macros the sources do not reference are rejected: scripts/check_macros.sh)
 set -eu
 cd "$(dirname "$0")/.."
 name=$1; shift
@@ -10,6 +11,7 @@ H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wno-unused-function -Wno-unused-variable -Wno-bitwise-instead-of-logical"
 mkdir -p build/var
 SRC=${SRC:-locomaze}
+scripts/check_macros.sh ogbench_amd/csrc/$SRC.hip "$@"
 $H $F "$@" -c ogbench_amd/csrc/$SRC.hip -o build/var/${SRC}_$name.o
 objs=$(ls build/obj/*.o | grep -v "/$SRC\.o" | tr '\n' ' ')
 mkdir -p _abx

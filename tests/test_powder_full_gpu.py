@@ -11,6 +11,7 @@ import pytest
 import torch
 
 import ogbench_amd
+from ogbench_amd import _lib
 from oracle import powder_full_np as orc
 
 pytestmark = pytest.mark.gpu
@@ -348,7 +349,7 @@ def test_render_cache_paths_agree(gpu, ne, size):
     acts = rng.randint(0, max(ne, a._xy_action_size) + 1, size=(K, n))
     for t in range(K):
         oa, ra, *_ = a.step(acts[t])  # cache path on render-only steps
-        b.world_full()  # b renders every step from the state
+        b._state_views()  # a writable hand-out: b renders every step from the state
         ob, rb, *_ = b.step(acts[t])
         assert torch.equal(oa, ob) and torch.equal(ra, rb), t
         if t > T:
@@ -357,6 +358,45 @@ def test_render_cache_paths_agree(gpu, ne, size):
         if t == T:
             assert bool(((a._scalar_view("ctrl") & 3) != 2).any())  # the next step has render-only envs
             c.load_state_dict(a.state_dict())  # c's cache still holds its own worlds' colours
+    for k in ('world', 'momentum', 'velocity'):
+        assert torch.equal(a.state_dict()[k], c.state_dict()[k]), k
+
+
+def test_kept_pointer_write_and_read_only_views(gpu):
+    """a host that keeps the writable world pointer and writes
+    through it after later steps announces the write with
+    ogbx_powder_state_written; readers use the const view
+    (ogbx_powder_state_view), which keeps the render cache.  The env written
+    through its kept pointer steps bit-identically to one restored with
+    load_state_dict, and world_ids / world_full read every step leave the
+    observations unchanged."""
+    n, K, T = 8, 24, 10
+    a, c, d = (_env(gpu, n, ne=5, size=64, max_episode_steps=50, auto_reset=True) for _ in range(3))
+    opts = dict(task_id=torch.arange(n, device=gpu) % 5 + 1)
+    a.reset(seed=3, options=opts)
+    c.reset(seed=3, options=opts)
+    d.reset(seed=77, options=dict(task_id=2))
+    w_keep = a._state_views()[0]  # writable, kept across steps
+    m_keep, v_keep, _ = a._full_views()
+    rng = np.random.RandomState(8)
+    acts = rng.randint(0, max(5, a._xy_action_size) + 1, size=(K, n))
+    for t in range(K):
+        ids_before = a.world_ids().clone()
+        full_before = a.world_full()
+        oa, ra, *_ = a.step(acts[t])
+        oc, rc, *_ = c.step(acts[t])
+        assert torch.equal(oa, oc) and torch.equal(ra, rc), t
+        assert torch.equal(ids_before, (full_before[:, 0]).to(torch.uint8)), t
+        if t == T:
+            assert bool(((a._scalar_view("ctrl") & 3) != 2).any())  # the next step has render-only envs
+            other = d.state_dict()
+            sd = a.state_dict()
+            sd.update(world=other['world'], momentum=other['momentum'], velocity=other['velocity'])
+            c.load_state_dict(sd)
+            w_keep.copy_(other['world'])  # through the pointers a handed out before the steps
+            m_keep.copy_(other['momentum'])
+            v_keep.copy_(other['velocity'])
+            _lib.check(_lib.lib().ogbx_powder_state_written(a._h))
     for k in ('world', 'momentum', 'velocity'):
         assert torch.equal(a.state_dict()[k], c.state_dict()[k]), k
 
