@@ -489,6 +489,7 @@ def bench_gcsample(args, world, rank, dev):
     if 'OGBX_GC_LOOKAHEAD' in os.environ:  # A/B knob (the sampler's lookahead config key)
         cfg['lookahead'] = os.environ['OGBX_GC_LOOKAHEAD'] != '0'
     gc = GCDataset(Dataset(data, device=dev), cfg, seed=rank)
+    gc_kernel = 'gc_ahead_kernel' if gc._lookahead else 'gc_sample_kernel'  # the launch of a steady call
     B = 1024
     batch = gc.sample(B)
 
@@ -530,8 +531,8 @@ def bench_gcsample(args, world, rank, dev):
         config=dict(workload='humanoidmaze-large-navigate-v0 offline replay', rows=R, batch=B,
                     agent_config='gciql humanoid (discount 0.995)', parallelism=f'replica x{world}'),
         # B = 1024 is a chain of HBM round trips (index loads, then rows), DESIGN 4.4
-        roofline=dict(bound='latency', kernel='gc_sample_kernel', achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
-                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic('gc_sample_kernel', 'gcsample', B, world),
+        roofline=dict(bound='latency', kernel=gc_kernel, achieved=achieved, peak=HBM_PEAK_GBS, unit='GB/s',
+                      frac=achieved / HBM_PEAK_GBS, traffic=_traffic(gc_kernel, 'gcsample', B, world),
                       kernel_ms=kern_ms, **kern_info, alg_bytes_per_launch=per_sample * B),
         extra=extra,
     )

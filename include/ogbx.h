@@ -34,8 +34,8 @@ extern "C" {
 
 /* History: 4 = rounds 1-3; 5 adds ogbx_gc_sample_ahead, ogbx_hgc_sample_ahead,
  * ogbx_maze_set_seed, ogbx_powder_set_seed, ogbx_stream_version,
- * ogbx_powder_state_view and ogbx_powder_state_written (no entry point of 4
- * changed its signature or meaning). */
+ * ogbx_powder_state_view, ogbx_powder_state_written and the sampler plans
+ * ogbx_gc_plan_* (no entry point of 4 changed its signature or meaning). */
 #define OGBX_ABI_VERSION 5
 
 typedef enum {
@@ -494,6 +494,44 @@ ogbx_status ogbx_hgc_sample_ahead(const ogbx_gc_buffer* buf, const ogbx_gc_confi
                                   int64_t batch, int64_t num_batches, uint64_t seed, uint64_t call_index,
                                   const int64_t* ahead_in, int64_t* ahead_out, const ogbx_hgc_outputs* out,
                                   void* stream);
+
+/* ---- Sampler plans: the steady sample(batch) call, prepared once ---------
+ * A plan holds what every call of one GCDataset / HGCDataset repeats -- the
+ * validated buffer and config, the Philox key of `seed`, the geometric log
+ * terms -- plus up to OGBX_GC_PLAN_SLOTS prepared output batches and the
+ * look-ahead state that ogbx_gc_sample_ahead leaves to its caller: one pair
+ * of selector buffers per stream (owned by the plan, allocated on the
+ * stream's first call, at most 8 streams; further streams run without
+ * look-ahead) and the (stream, samples, call) the stored selectors belong
+ * to.  So a host that calls ogbx_gc_plan_sample with increasing call indices
+ * gets the look-ahead's latency without keeping its contract, and a call
+ * whose index, size or stream does not match simply computes its own
+ * selectors.  Every output is bit-identical to ogbx_gc_sample /
+ * ogbx_hgc_sample with the same seed and call_index (whatever the slot,
+ * stream or look-ahead setting).  hcfg NULL: GCDataset; else HGCDataset.
+ * lookahead 0: every call launches the direct kernel. */
+#define OGBX_GC_PLAN_SLOTS 8
+typedef struct ogbx_gc_plan_s* ogbx_gc_plan_t;
+ogbx_status ogbx_gc_plan_create(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                                const ogbx_hgc_config* hcfg, uint64_t seed, int32_t lookahead,
+                                ogbx_gc_plan_t* plan);
+/* Prepare output batch `slot` (0..7): the columns (select codes as
+ * ogbx_gc_sample / ogbx_hgc_sample), batch x num_batches samples, and the
+ * scalar outputs (GC: idxs / goals may be NULL, masks and rewards not; HGC:
+ * hgc_out, the GC scalars unused).  Overwrites the slot; launches already
+ * issued keep their arguments. */
+ogbx_status ogbx_gc_plan_set_batch(ogbx_gc_plan_t plan, int32_t slot, const ogbx_gc_column* cols,
+                                   int32_t num_cols, int64_t batch, int64_t num_batches, int64_t* idxs_out,
+                                   int64_t* value_goal_out, int64_t* actor_goal_out, double* masks,
+                                   double* rewards, const ogbx_hgc_outputs* hgc_out);
+/* One sample() call into the batch of `slot`, Philox counter call_index, on
+ * `stream`: the look-ahead kernel (batch x num_batches <= 1024) or the direct
+ * kernel. */
+ogbx_status ogbx_gc_plan_sample(ogbx_gc_plan_t plan, int32_t slot, uint64_t call_index, void* stream);
+/* Calls served from selectors a previous launch stored (diagnostic). */
+int64_t ogbx_gc_plan_hits(ogbx_gc_plan_t plan);
+/* Frees the plan and its look-ahead buffers (waits for launches in flight). */
+ogbx_status ogbx_gc_plan_destroy(ogbx_gc_plan_t plan);
 
 /* traj_end[r] = terminal_locs[searchsorted(terminal_locs, r, 'left')] for
  * r in [0, R): binary search per row over the sorted terminal_locs

@@ -1037,6 +1037,230 @@ ogbx_status ogbx_hgc_sample_ahead(const ogbx_gc_buffer* buf, const ogbx_gc_confi
   return OGBX_OK;
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------- sampler plans
+// A plan owns everything a steady stream of GCDataset / HGCDataset.sample
+// calls repeats: the validated buffer and config, the Philox key, the
+// geometric log terms, up to OGBX_GC_PLAN_SLOTS prepared output batches (the
+// column descriptors as one kernel-argument image), and the look-ahead state:
+// one pair of selector buffers per stream (allocated on the stream's first
+// call, never shared across streams) and the (stream, samples, call) the
+// last launch stored selectors for.  A call is then one lookup and one launch.
+namespace {
+constexpr int kPlanStreams = 8;
+
+struct PlanBatch {
+  bool set = false;
+  GcColumns cc{};
+  int32_t ncols = 0;
+  int64_t batch = 0, nb = 0;
+  int64_t *idxs = nullptr, *vg = nullptr, *ag = nullptr;
+  double *masks = nullptr, *rewards = nullptr;
+  ogbx_hgc_outputs hout{};
+  bool flat4 = false;
+};
+
+struct PlanPair {
+  void* stream = nullptr;
+  int64_t* buf[2] = {nullptr, nullptr};
+};
+}  // namespace
+
+struct ogbx_gc_plan_s {
+  ogbx_gc_buffer buf;
+  ogbx_gc_config cfg;
+  ogbx_hgc_config hcfg;
+  bool hgc = false, lookahead = true;
+  int device = 0;
+  uint32_t k0 = 0, k1 = 0;
+  double v_log_q = 0, a_log_q = 0, l_log_q = 0;
+  PlanBatch slots[OGBX_GC_PLAN_SLOTS];
+  PlanPair pairs[kPlanStreams];
+  int npairs = 0;
+  // the selectors in pairs[key_pair].buf[key_which] belong to (key_total, key_call)
+  bool key_valid = false;
+  int key_pair = 0, key_which = 0;
+  int64_t key_total = 0;
+  uint64_t key_call = 0;
+  int64_t hits = 0;
+};
+
+extern "C" {
+
+ogbx_status ogbx_gc_plan_create(const ogbx_gc_buffer* buf, const ogbx_gc_config* cfg,
+                                const ogbx_hgc_config* hcfg, uint64_t seed, int32_t lookahead,
+                                ogbx_gc_plan_t* plan) {
+  OGBX_CHECK(buf && cfg && plan, OGBX_EINVAL, "ogbx_gc_plan_create: null argument");
+  OGBX_CHECK(buf->num_rows > 0 && buf->traj_end, OGBX_EINVAL, "empty trajectory buffer");
+  OGBX_CHECK(buf->valid_idxs == nullptr || buf->num_valid > 0, OGBX_EINVAL, "no valid transitions in the dataset");
+  OGBX_CHECK(periodic_ok(*buf), OGBX_EINVAL, "ogbx_gc_buffer: inconsistent period fields");
+  if (hcfg) {
+    OGBX_CHECK(hcfg->hv_mask_table && hcfg->hv_reward_table && hcfg->lv_mask_table && hcfg->lv_reward_table,
+               OGBX_EINVAL, "ogbx_gc_plan_create: missing reward/mask tables");
+    OGBX_CHECK(hcfg->value_subgoal_steps >= 0 && hcfg->low_subgoal_steps >= 0 && hcfg->actor_subgoal_steps >= 0,
+               OGBX_EINVAL, "ogbx_gc_plan_create: negative subgoal steps");
+    OGBX_CHECK(!hcfg->has_low_value_goals || (hcfg->low_discount > 0.0 && hcfg->low_discount < 1.0), OGBX_EINVAL,
+               "ogbx_gc_plan_create: low_discount must be in (0, 1)");
+  }
+  auto* p = new (std::nothrow) ogbx_gc_plan_s();
+  OGBX_CHECK(p, OGBX_ENOMEM, "ogbx_gc_plan_create: out of host memory");
+  p->buf = *buf;
+  p->cfg = *cfg;
+  p->hgc = hcfg != nullptr;
+  if (hcfg) p->hcfg = *hcfg;
+  p->lookahead = lookahead != 0;
+  if (hipGetDevice(&p->device) != hipSuccess) p->device = 0;
+  seed_key(seed, p->hgc ? kTagHgcSample : kTagGcSample, &p->k0, &p->k1);
+  p->v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
+  p->a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
+  p->l_log_q = (hcfg && hcfg->has_low_value_goals) ? std::log(1.0 - (1.0 - hcfg->low_discount)) : 0.0;
+  *plan = p;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_gc_plan_set_batch(ogbx_gc_plan_t p, int32_t slot, const ogbx_gc_column* cols, int32_t num_cols,
+                                   int64_t batch, int64_t num_batches, int64_t* idxs_out, int64_t* value_goal_out,
+                                   int64_t* actor_goal_out, double* masks, double* rewards,
+                                   const ogbx_hgc_outputs* hgc_out) {
+  OGBX_CHECK(p, OGBX_EINVAL, "null plan");
+  OGBX_CHECK(slot >= 0 && slot < OGBX_GC_PLAN_SLOTS, OGBX_EINVAL, "ogbx_gc_plan_set_batch: slot out of range");
+  OGBX_CHECK(num_cols >= 0 && num_cols <= kGcMaxCols, OGBX_EINVAL, "ogbx_gc_plan_set_batch: at most 32 columns");
+  OGBX_CHECK(batch > 0 && num_batches > 0, OGBX_EINVAL, "batch and num_batches must be > 0");
+  if (p->hgc) {
+    OGBX_CHECK(hgc_out && hgc_out->high_value_offsets && hgc_out->high_value_subgoal_steps &&
+                   hgc_out->high_value_masks && hgc_out->high_value_rewards && hgc_out->low_value_subgoal_steps &&
+                   hgc_out->low_value_masks && hgc_out->low_value_rewards && hgc_out->masks && hgc_out->rewards,
+               OGBX_EINVAL, "ogbx_gc_plan_set_batch: missing HGC scalar output");
+  } else {
+    OGBX_CHECK(masks && rewards, OGBX_EINVAL, "ogbx_gc_plan_set_batch: null masks / rewards");
+  }
+  PlanBatch b;
+  const int max_sel = p->hgc ? kHgcSel - 1 : 3;
+  for (int i = 0; i < num_cols; ++i) {
+    OGBX_CHECK(cols[i].src_stride == 0 || cols[i].src_stride >= cols[i].row_bytes, OGBX_EINVAL,
+               "ogbx_gc_plan_set_batch: src_stride below row_bytes");
+    OGBX_CHECK(cols[i].src && cols[i].dst && cols[i].row_bytes > 0 && cols[i].select >= 0 &&
+                   cols[i].select <= max_sel,
+               OGBX_EINVAL, "ogbx_gc_plan_set_batch: bad column descriptor");
+    b.cc.c[i] = cols[i];
+  }
+  b.ncols = num_cols;
+  b.batch = batch;
+  b.nb = num_batches;
+  b.idxs = idxs_out;
+  b.vg = value_goal_out;
+  b.ag = actor_goal_out;
+  b.masks = masks;
+  b.rewards = rewards;
+  if (hgc_out) b.hout = *hgc_out;
+  b.flat4 = flat4_columns(b.cc, num_cols);
+  b.set = true;
+  p->slots[slot] = b;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_gc_plan_sample(ogbx_gc_plan_t p, int32_t slot, uint64_t call_index, void* stream) {
+  OGBX_CHECK(p && slot >= 0 && slot < OGBX_GC_PLAN_SLOTS && p->slots[slot].set, OGBX_EINVAL,
+             "ogbx_gc_plan_sample: no batch in this slot");
+  const PlanBatch& b = p->slots[slot];
+  const int64_t total = b.batch * b.nb;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t clo = (uint32_t)call_index, chi = (uint32_t)(call_index >> 32);
+  if (!p->lookahead || total > kGcAheadMaxSamples) {
+    p->key_valid = false;
+    int64_t tile = total / 1024;  // as ogbx_gc_sample
+    if (tile < 1) tile = 1;
+    if (tile > kGcMaxTile) tile = kGcMaxTile;
+    const int64_t blocks = (total + tile - 1) / tile;
+    const bool f4 = tile <= 4 && b.flat4;
+    if (p->hgc) {
+      hipLaunchKernelGGL(hgc_sample_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, p->buf, p->cfg, p->hcfg,
+                         b.cc, b.ncols, total, (int)tile, ogbx_hgc_draws{}, p->k0, p->k1, clo, chi, p->v_log_q,
+                         p->a_log_q, p->l_log_q, b.hout, ogbx_hgc_draw_record{}, f4);
+      OGBX_LAUNCHED("hgc_sample_kernel");
+    } else {
+      hipLaunchKernelGGL(gc_sample_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, s, p->buf, p->cfg, b.cc,
+                         b.ncols, total, (int)tile, ogbx_gc_draws{}, p->k0, p->k1, clo, chi, p->v_log_q, p->a_log_q,
+                         b.idxs, b.vg, b.ag, b.masks, b.rewards, ogbx_gc_draw_record{}, f4);
+      OGBX_LAUNCHED("gc_sample_kernel");
+    }
+    return OGBX_OK;
+  }
+  // this stream's buffer pair (allocated on its first call; with every pair
+  // taken, the call runs without look-ahead: nothing stored, nothing read)
+  int pi = -1;
+  for (int i = 0; i < p->npairs; ++i)
+    if (p->pairs[i].stream == stream) pi = i;
+  if (pi < 0 && p->npairs < kPlanStreams) {
+    const size_t words = (size_t)kGcAheadMaxSamples * (p->hgc ? kHgcAheadWords : kGcAheadWords);
+    int cur = 0;
+    OGBX_HIP(hipGetDevice(&cur));
+    if (cur != p->device) OGBX_HIP(hipSetDevice(p->device));
+    PlanPair pr;
+    pr.stream = stream;
+    hipError_t e0 = hipMalloc(&pr.buf[0], words * sizeof(int64_t));
+    hipError_t e1 = e0 == hipSuccess ? hipMalloc(&pr.buf[1], words * sizeof(int64_t)) : e0;
+    if (cur != p->device) (void)hipSetDevice(cur);
+    if (e0 != hipSuccess || e1 != hipSuccess) {
+      if (pr.buf[0]) (void)hipFree(pr.buf[0]);
+      return hip_fail(e0 != hipSuccess ? e0 : e1, "hipMalloc (look-ahead buffers)");
+    }
+    pi = p->npairs++;
+    p->pairs[pi] = pr;
+  }
+  const int64_t* in = nullptr;
+  int64_t* out = nullptr;
+  int which = 0;
+  if (pi >= 0) {
+    const bool hit = p->key_valid && p->key_pair == pi && p->key_total == total && p->key_call == call_index;
+    if (hit) {
+      in = p->pairs[pi].buf[p->key_which];
+      which = 1 - p->key_which;
+      ++p->hits;
+    }
+    out = p->pairs[pi].buf[which];
+  }
+  const uint64_t next = call_index + 1;
+  if (p->hgc) {
+    hipLaunchKernelGGL(hgc_ahead_kernel, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, p->hcfg, b.cc,
+                       b.ncols, p->k0, p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q,
+                       p->a_log_q, p->l_log_q, in, out, b.hout, b.flat4);
+    OGBX_LAUNCHED("hgc_ahead_kernel");
+  } else {
+    hipLaunchKernelGGL(gc_ahead_kernel, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, b.cc, b.ncols,
+                       p->k0, p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q, p->a_log_q, in,
+                       out, b.idxs, b.vg, b.ag, b.masks, b.rewards, b.flat4);
+    OGBX_LAUNCHED("gc_ahead_kernel");
+  }
+  p->key_valid = pi >= 0;
+  p->key_pair = pi;
+  p->key_which = which;
+  p->key_total = total;
+  p->key_call = next;
+  return OGBX_OK;
+}
+
+int64_t ogbx_gc_plan_hits(ogbx_gc_plan_t p) { return p ? p->hits : -1; }
+
+ogbx_status ogbx_gc_plan_destroy(ogbx_gc_plan_t p) {
+  if (!p) return OGBX_OK;
+  hipError_t err = hipSuccess;
+  for (int i = 0; i < p->npairs; ++i)
+    for (int k = 0; k < 2; ++k)
+      if (p->pairs[i].buf[k]) {
+        const hipError_t e = hipFree(p->pairs[i].buf[k]);  // waits for in-flight launches
+        if (err == hipSuccess) err = e;
+      }
+  delete p;
+  if (err != hipSuccess) return hip_fail(err, "hipFree (look-ahead buffers)");
+  return OGBX_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
 ogbx_status ogbx_gc_traj_end(const int64_t* terminal_locs, int64_t num_terminals,
                              int64_t num_rows, int64_t* traj_end, void* stream) {
   OGBX_CHECK(terminal_locs && traj_end && num_terminals > 0 && num_rows > 0, OGBX_EINVAL,

@@ -20,6 +20,7 @@ injected bit-exactly through ``draws=`` for parity tests.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import numpy as np
 
@@ -139,6 +140,19 @@ def _bind():
             ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
         ]
+        L.ogbx_gc_plan_create.restype = ctypes.c_int32
+        L.ogbx_gc_plan_create.argtypes = [P(GcBuffer), P(GcConfig), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32,
+                                          P(ctypes.c_void_p)]
+        L.ogbx_gc_plan_set_batch.restype = ctypes.c_int32
+        L.ogbx_gc_plan_set_batch.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
+                                             ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.ogbx_gc_plan_sample.restype = ctypes.c_int32
+        L.ogbx_gc_plan_sample.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_void_p]
+        L.ogbx_gc_plan_hits.restype = ctypes.c_int64
+        L.ogbx_gc_plan_hits.argtypes = [ctypes.c_void_p]
+        L.ogbx_gc_plan_destroy.restype = ctypes.c_int32
+        L.ogbx_gc_plan_destroy.argtypes = [ctypes.c_void_p]
         L.ogbx_gc_traj_end.restype = ctypes.c_int32
         L.ogbx_gc_traj_end.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                        ctypes.c_void_p]
@@ -162,12 +176,6 @@ def nonzero_positive(x):
     _lib.check(L.ogbx_nonzero_f32(_lib.ptr(x), x.numel(), _lib.ptr(out), _lib.ptr(cnt),
                                   _lib.stream_of(x.device)))
     return out[: int(cnt.item())]
-
-
-def _skey(stream):
-    """A stream handle as a hashable, comparable key (ctypes.c_void_p
-    objects compare by identity, so two handles of one stream never match)."""
-    return stream.value if isinstance(stream, ctypes.c_void_p) else stream
 
 
 def _to_device(v, device):
@@ -249,8 +257,8 @@ class GCDataset:
     p_trajgoal, p_randomgoal, geom_sample, gc_negative, p_aug, frame_stack;
     and two of this sampler's own: row_record (default True; False skips the
     interleaved copy of the small columns, ``_row_record``) and lookahead
-    (True: each call also computes the next equal call's selectors,
-    ``_launch_plain``; default False for GCDataset, True for HGCDataset).
+    (default True: each plain call of <= 1,024 samples also computes the next
+    call's selectors, so the next call only gathers; ``ogbx_gc_plan_*``).
     """
 
     def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None, _plain=False):
@@ -314,12 +322,14 @@ class GCDataset:
         self._seed = int(seed) if seed is not None else None
         self._calls = 0
         self._out_cache = {}
-        # look-ahead (ogbx_gc_sample_ahead): two ping-pong selector buffers and
-        # the (batch, num_batches, stream, call) whose selectors one of them holds
+        # plain (Philox, no idxs / draws / recording) calls go through a sampler
+        # plan (ogbx_gc_plan_*): the prepared output batches and the look-ahead
+        # state live in libogbx, so a steady call is one lookup and one launch
         self._lookahead = bool(config.get('lookahead', self._LOOKAHEAD_DEFAULT))
-        self._ahead_bufs = None
-        self._ahead = None
-        self.ahead_hits = 0  # calls whose selectors the previous launch stored (diagnostic)
+        self._plan = None
+        self._plan_seed = None
+        self._plan_final = None
+        self._slot = 0
 
     # ---------------------------------------------------------------- helpers
     _RECORD_MAX = 128  # one L2 line
@@ -436,63 +446,42 @@ class GCDataset:
             add(goal_src, 'actor_goals', 3)
         return out, cols
 
-    _AHEAD_MAX = 1024  # samples per call the look-ahead kernel takes (one per workgroup)
-    # GC: measured neutral (5.99 vs 5.94 us per B = 1,024 call: the stored
-    # selectors' load costs about what the short GC draw chain did), so off by
-    # default; HGC's longer chain gains (8.05 vs 8.38 us), on by default
-    _LOOKAHEAD_DEFAULT = False
-    _AHEAD_WORDS = 8   # OGBX_GC_AHEAD_WORDS
-    _HGC_AHEAD_WORDS = 20  # OGBX_HGC_AHEAD_WORDS
+    # GC: with the look-ahead actually hitting (round 5), 4.7 vs 5.8 us per
+    # B = 1,024 launch back to back (profiles/r05_gcsample_*), so on by
+    # default for both samplers
+    _LOOKAHEAD_DEFAULT = True
 
-    _AHEAD_STREAMS = 8  # streams with a buffer pair of their own before the pairs are recycled
+    def _hcfg_ptr(self):
+        return None  # GCDataset; HGCDataset passes its ogbx_hgc_config
 
-    def _ahead_slots(self, B, nb, stream, call, words):
-        """(ahead_in, ahead_out, index of ahead_out) for call `call`: the
-        selectors stored by the previous launch when it stored them for exactly
-        this (batch, num_batches, stream, call), else none (computed in line).
+    def _plan_for(self, seed):
+        """The sampler plan of this (dataset, config, seed), created on the
+        first plain call (the seed is drawn then if none was given)."""
+        if self._plan is None or self._plan_seed != seed:
+            self._drop_plan()
+            L = self._L
+            h = ctypes.c_void_p()
+            _lib.check(L.ogbx_gc_plan_create(self._buf, self._cfg, self._hcfg_ptr(), seed, int(self._lookahead),
+                                             ctypes.byref(h)), 'gc_plan_create')
+            self._plan, self._plan_seed = h.value, seed
+            self._plan_final = weakref.finalize(self, L.ogbx_gc_plan_destroy, h.value)
+            self._out_cache.clear()  # their slots belong to the old plan
+        return self._plan
 
-        Every stream has its own ping-pong pair, allocated on (and so only
-        ever reused in the order of) that stream: a launch on another stream
-        never writes a buffer a launch still in flight on this one reads or
-        writes."""
-        key = _skey(stream)
-        if self._ahead_bufs is None:
-            self._ahead_bufs = {}
-        pair = self._ahead_bufs.get(key)
-        if pair is None or pair[0][0].numel() < self._AHEAD_MAX * words:
-            torch = _torch()
-            if len(self._ahead_bufs) >= self._AHEAD_STREAMS:
-                # the caching allocator hands a freed block out again only in
-                # its stream's order, so dropping a pair is stream-safe
-                self._ahead_bufs.clear()
-                self._ahead = None
-            bufs = [torch.empty(self._AHEAD_MAX * words, dtype=torch.int64, device=self.device) for _ in range(2)]
-            pair = self._ahead_bufs[key] = (bufs, [t.data_ptr() for t in bufs])
-            if self._ahead is not None and self._ahead[0][2] == key:
-                self._ahead = None
-        ptrs = pair[1]
-        a = self._ahead
-        if a is not None and a[0] == (B, nb, key, call):
-            self.ahead_hits += 1
-            return ptrs[a[1]], ptrs[1 - a[1]], 1 - a[1]
-        return None, ptrs[0], 0
+    def _drop_plan(self):
+        if self._plan_final is not None:
+            self._plan_final()
+        self._plan, self._plan_final = None, None
 
-    def _launch_plain(self, col_p, ncols, B, nb, seed, call, idx_p, vg_p, ag_p, masks_p, rewards_p, stream):
-        """One Philox-mode GCDataset.sample launch.  Small calls (<= 1024
-        samples) go through the look-ahead kernel: this launch gathers from
-        the selectors the previous equal call stored (when it stored them for
-        exactly this call) and stores the next call's; results are
-        bit-identical either way."""
-        total = B * nb
-        if not self._lookahead or total > self._AHEAD_MAX:
-            self._ahead = None
-            return self._L.ogbx_gc_sample(self._buf, self._cfg, col_p, ncols, B, nb, None, seed, call, idx_p, vg_p,
-                                          ag_p, masks_p, rewards_p, None, stream)
-        src, dst, which = self._ahead_slots(B, nb, stream, call, self._AHEAD_WORDS)
-        st = self._L.ogbx_gc_sample_ahead(self._buf, self._cfg, col_p, ncols, B, nb, seed, call, src, dst, idx_p,
-                                          vg_p, ag_p, masks_p, rewards_p, stream)
-        self._ahead = ((B, nb, _skey(stream), call + 1), which) if st == 0 else None
-        return st
+    @property
+    def ahead_hits(self):
+        """Calls served from selectors the previous launch stored (diagnostic)."""
+        return int(self._L.ogbx_gc_plan_hits(self._plan)) if self._plan is not None else 0
+
+    def _next_slot(self):
+        slot = self._slot
+        self._slot = (slot + 1) % 8  # OGBX_GC_PLAN_SLOTS; the out cache holds at most the last two
+        return slot
 
     def sample(self, batch_size, idxs=None, evaluation=False, draws=None, record_draws=False,
                num_batches=1, _keys=None, out=None):
@@ -515,11 +504,12 @@ class GCDataset:
             self._refresh_record()
         if out is not None and plain_call:
             hit = self._out_cache.get(id(out))
-            if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
-                col_p, ncols, idx_p, masks_p, rewards_p = hit[2]
+            if (hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches))
+                    and self._plan_seed == self._seed):
                 seed, call = self._next_seed()
-                _lib.check(self._launch_plain(col_p, ncols, int(batch_size), int(num_batches), seed, call, idx_p, None,
-                                              None, masks_p, rewards_p, _lib.stream_of(self.device)), 'gc_sample')
+                st = self._L.ogbx_gc_plan_sample(self._plan, hit[2], call, _lib.stream_of(self.device))
+                if st:
+                    _lib.check(st, 'gc_sample')
                 self._p_aug_draw(out, evaluation)
                 return out
         out, cols = self._columns(total, _keys)
@@ -553,10 +543,15 @@ class GCDataset:
                                     device=self.device) for k in _DRAW_ORDER}
             rec = GcDrawRecord(*[rec_t[k].data_ptr() for k in _DRAW_ORDER])
         seed, call = self._next_seed()
+        slot = None
         if plain_call:
-            st = self._launch_plain(ctypes.cast(col_arr, ctypes.c_void_p), len(cols), int(batch_size),
-                                    int(num_batches), seed, call, _lib.ptr(idx_out), _lib.ptr(vg), _lib.ptr(ag),
-                                    _lib.ptr(masks), _lib.ptr(rewards), _lib.stream_of(self.device))
+            plan = self._plan_for(seed)
+            slot = self._next_slot()
+            _lib.check(self._L.ogbx_gc_plan_set_batch(plan, slot, ctypes.cast(col_arr, ctypes.c_void_p), len(cols),
+                                                      int(batch_size), int(num_batches), _lib.ptr(idx_out),
+                                                      _lib.ptr(vg), _lib.ptr(ag), _lib.ptr(masks),
+                                                      _lib.ptr(rewards), None), 'gc_plan_set_batch')
+            st = self._L.ogbx_gc_plan_sample(plan, slot, call, _lib.stream_of(self.device))
         else:
             st = self._L.ogbx_gc_sample(
                 self._buf, self._cfg, ctypes.cast(col_arr, ctypes.c_void_p), len(cols), int(batch_size),
@@ -569,14 +564,11 @@ class GCDataset:
             out['masks'] = masks
             out['rewards'] = rewards
         if plain_call:
-            # remember the descriptors so that sample(..., out=this) skips setup
+            # remember the batch's plan slot so that sample(..., out=this) skips
+            # setup (the output tensors stay alive in `out`)
             if len(self._out_cache) >= 2:
                 self._out_cache.clear()
-            # (the output tensors stay alive in `out`; col_arr is kept for its pointer)
-            fast = (ctypes.cast(col_arr, ctypes.c_void_p), len(cols), _lib.ptr(idx_out), _lib.ptr(masks),
-                    _lib.ptr(rewards))
-            self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), fast, col_arr, masks, rewards,
-                                        idx_out)
+            self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), slot, masks, rewards, idx_out)
         if self._plain:
             return out
         self._p_aug_draw(out, evaluation)
@@ -668,7 +660,8 @@ class HGCDataset(GCDataset):
     per sample() returns the reference's 27 (28 with low_discount) keys.
     """
 
-    _LOOKAHEAD_DEFAULT = True
+    def _hcfg_ptr(self):
+        return ctypes.byref(self._hcfg)
 
     def __init__(self, dataset, config, preprocess_frame_stack=True, seed=None):
         super().__init__(dataset, config, preprocess_frame_stack=preprocess_frame_stack, seed=seed)
@@ -744,9 +737,14 @@ class HGCDataset(GCDataset):
         if self._rec_src:
             self._refresh_record()
         hit = self._out_cache.get(id(out)) if (out is not None and plain_call) else None
-        if hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches)):
-            _, _, col_arr, ncols, outs, _ = hit
-            dr, rec, keep = None, None, []
+        if (hit is not None and hit[0] is out and hit[1] == (int(batch_size), int(num_batches))
+                and self._plan_seed == self._seed):
+            seed, call = self._next_seed()
+            st = self._Lh.ogbx_gc_plan_sample(self._plan, hit[2], call, _lib.stream_of(self.device))
+            if st:
+                _lib.check(st, 'hgc_sample')
+            self._p_aug_draw(out, evaluation)
+            return out
         else:
             out, cols = self._hcolumns(total)
             col_keep = (GcColumn * max(1, len(cols)))(*cols)
@@ -777,20 +775,19 @@ class HGCDataset(GCDataset):
                 idx_t = {k: torch.empty(total, dtype=torch.int64, device=self.device) for k in _HGC_SCALARS[:4]}
                 for k, t in idx_t.items():
                     setattr(outs, k, t.data_ptr())
-            if plain_call:
-                if len(self._out_cache) >= 2:
-                    self._out_cache.clear()
-                self._out_cache[id(out)] = (out, (int(batch_size), int(num_batches)), col_arr, ncols, outs, col_keep)
         seed, call = self._next_seed()
         stream = _lib.stream_of(self.device)
         B, nb = int(batch_size), int(num_batches)
-        if plain_call and self._lookahead and B * nb <= self._AHEAD_MAX:
-            src, dst, which = self._ahead_slots(B, nb, stream, call, self._HGC_AHEAD_WORDS)
-            st = self._Lh.ogbx_hgc_sample_ahead(self._buf, self._cfg, self._hcfg, col_arr, ncols, B, nb, seed, call,
-                                                src, dst, outs, stream)
-            self._ahead = ((B, nb, _skey(stream), call + 1), which) if st == 0 else None
+        if plain_call:
+            plan = self._plan_for(seed)
+            slot = self._next_slot()
+            _lib.check(self._Lh.ogbx_gc_plan_set_batch(plan, slot, col_arr, ncols, B, nb, None, None, None, None,
+                                                       None, ctypes.byref(outs)), 'gc_plan_set_batch')
+            if len(self._out_cache) >= 2:
+                self._out_cache.clear()
+            self._out_cache[id(out)] = (out, (B, nb), slot, outs, col_keep)
+            st = self._Lh.ogbx_gc_plan_sample(plan, slot, call, stream)
         else:
-            self._ahead = None
             st = self._Lh.ogbx_hgc_sample(self._buf, self._cfg, self._hcfg, col_arr, ncols, B, nb, dr, seed, call,
                                           outs, rec, stream)
         _lib.check(st, 'hgc_sample')

@@ -43,6 +43,8 @@ ABI5_SYMBOLS = {
     # offline replay
     'ogbx_gc_sample', 'ogbx_gc_sample_ahead', 'ogbx_hgc_sample', 'ogbx_hgc_sample_ahead', 'ogbx_gc_traj_end',
     'ogbx_nonzero_f32', 'ogbx_compact_terminals', 'ogbx_gather_rows', 'ogbx_relabel_maze',
+    'ogbx_gc_plan_create', 'ogbx_gc_plan_set_batch', 'ogbx_gc_plan_sample', 'ogbx_gc_plan_hits',
+    'ogbx_gc_plan_destroy',
     # evaluation + collective
     'ogbx_eval_accumulate', 'ogbx_comm_unique_id', 'ogbx_comm_create', 'ogbx_comm_destroy', 'ogbx_eval_allgather',
 }

@@ -10,6 +10,8 @@ import numpy as np
 import pytest
 import torch
 
+from ogbench_amd import _lib
+
 from ogbench_amd.datasets import Dataset, GCDataset, nonzero_positive
 from oracle import gcdataset_np as orc
 
@@ -317,7 +319,7 @@ def test_lookahead_matches_direct_sampling(gpu, gold):
                     assert torch.equal(x[k], y[k]), (cname, i, k)
             if mode != 'record':
                 prev_a, prev_b = x, y
-        assert a._ahead is not None  # the last calls ran ahead
+        assert a.ahead_hits > 0  # calls were served from stored selectors
     # Dataset.sample (plain sampler) and get_random_idxs
     d1, d2 = Dataset(data, device=gpu), Dataset(data, device=gpu)
     d1._sampler()._lookahead, d2._sampler()._lookahead = True, False
@@ -326,3 +328,45 @@ def test_lookahead_matches_direct_sampling(gpu, gold):
         x, y = d1.sample(512), d2.sample(512)
         for k in y:
             assert torch.equal(x[k], y[k]), k
+
+
+def test_raw_ahead_abi_matches_direct(gpu, gold):
+    """ogbx_gc_sample_ahead driven directly through the C-ABI as INTEGRATION.md
+    section 5 shows a non-Python host doing it (two caller-owned buffers that
+    alternate, ahead_in = NULL on the first call and after a call-index gap):
+    every batch bit-identical to ogbx_gc_sample with the same seed and call."""
+    import ctypes
+
+    from ogbench_amd import datasets as D
+
+    data = orc.load_dataset(_raw(gold), compact_dataset=True)
+    cfg = dict(CONFIGS['gciql'], p_aug=None, frame_stack=None, lookahead=False)
+    gc = GCDataset(Dataset(data, device=gpu), cfg, seed=31)
+    L = gc._L
+    B = 512
+    words = 8  # OGBX_GC_AHEAD_WORDS
+    bufs = [torch.empty(B * words, dtype=torch.int64, device=gpu) for _ in range(2)]
+    stream = _lib.stream_of(gpu)
+
+    def batch():
+        out, cols = gc._columns(B, None)
+        arr = (D.GcColumn * len(cols))(*cols)
+        m = torch.empty(B, dtype=torch.float64, device=gpu)
+        r = torch.empty(B, dtype=torch.float64, device=gpu)
+        return out, arr, m, r
+
+    prev = None
+    for call in [0, 1, 2, 3, 7, 8, 9]:
+        xa, arr_a, ma, ra = batch()
+        xb, arr_b, mb, rb = batch()
+        src = prev[1] if prev is not None and prev[0] == call else None
+        dst = bufs[call & 1]
+        _lib.check(L.ogbx_gc_sample_ahead(gc._buf, gc._cfg, ctypes.cast(arr_a, ctypes.c_void_p), len(arr_a), B, 1,
+                                          31, call, _lib.ptr(src), _lib.ptr(dst), None, None, None, _lib.ptr(ma),
+                                          _lib.ptr(ra), stream))
+        _lib.check(L.ogbx_gc_sample(gc._buf, gc._cfg, ctypes.cast(arr_b, ctypes.c_void_p), len(arr_b), B, 1, None,
+                                    31, call, None, None, None, _lib.ptr(mb), _lib.ptr(rb), None, stream))
+        prev = (call + 1, dst)
+        assert torch.equal(ma, mb) and torch.equal(ra, rb), call
+        for k in xa:
+            assert torch.equal(xa[k], xb[k]), (call, k)
