@@ -508,7 +508,17 @@ constexpr double kImpDelta = kPointModel.imp_dmax - kPointModel.imp_dmin;
 __device__ __forceinline__ double band_u(const PointModel& pm, double d) {
   const double x = fmin(fmax(fabs(d) * pm.inv_width, 0.0), 1.0);
   const double m = fmin(fmax(fma(2.0, x, -1.0), 0.0), 1.0);
+#ifdef OGBX_BAND_NO_OMOD
   return fma(m, m, fma(-(x + x), x, 2.0));
+#else
+  // 2 - 2x^2 as (1 - x^2) times 2 by the VOP3 output modifier: one
+  // instruction instead of an add and an fma, the same value (a power-of-two
+  // scale commutes with rounding; 1 - x^2 in [0, 1] is never subnormal
+  // unless zero)
+  double t;
+  asm("v_fma_f64 %0, %1, -%1, 1.0 mul:2" : "=v"(t) : "v"(x));
+  return fma(m, m, t);
+#endif
 }
 
 #ifdef OGBX_WAVE_STAMPS
@@ -714,6 +724,7 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
 #endif
     if (__builtin_expect(__any(!done), 0)) {
       OGBX_WPATH(0);
+#ifdef OGBX_ITER_PER_LANE
 #pragma unroll 1
       for (int it = 0; it < kLeanIters && !done; ++it) {
         OGBX_WPATH(20);
@@ -727,6 +738,29 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
         A2 = local_edge_mask(c, ux, uy);
         done = A2 == act;
       }
+#else
+      // Every lane runs the iteration (a wave-uniform loop): typically one or
+      // two lanes of the wave flip an edge, and gfx950 issues a dependent
+      // chain about twice as slowly with <= 8 active lanes, so
+      // the divergent per-lane loop ran at half speed.  A settled lane is at
+      // a fixed point (act == A2, pw = piece_weights(act)): its rerun
+      // recomputes the same ux, uy and A2 bit for bit, so every lane's result
+      // equals the per-lane loop's.
+#pragma unroll 1
+      for (int it = 0; it < kLeanIters; ++it) {
+        OGBX_WPATH(20);
+#ifdef OGBX_PHYS_STATS
+        if (!done) OGBX_STAT(4);
+        trips += !done;
+#endif
+        act = A2;
+        piece_weights(act, pw);
+        local_piece_min(c, pw, vsx, vsy, &ux, &uy);
+        A2 = local_edge_mask(c, ux, uy);
+        done = A2 == act;
+        if (!__any(!done)) break;
+      }
+#endif
       bl |= !done;
 #ifdef OGBX_PHYS_STATS
       if (trips == 1) OGBX_STAT(5);

@@ -20,3 +20,5 @@ print(f"{r['config']['workload']}: {r['value']/1e6:.1f} M/s, {r['ms_per_step']*1
 PY
 done
 bash scripts/gpu_r05_floor.sh
+[ "${AB:-1}" = 1 ] || exit 0
+ROUNDS=${ROUNDS:-2} bash scripts/gpu_maze_ab.sh
