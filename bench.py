@@ -252,6 +252,9 @@ def _maze_job(total, base, n, ring, dev, maze='large'):
     import ogbench_amd
 
     env = ogbench_amd.make(f'pointmaze-{maze}-v0', num_envs=n, device=dev, auto_reset=True, env_base=base)
+    if 'OGBX_EPW' in os.environ:  # A/B knob: envs per 64-lane wave (results do not depend on it)
+        from ogbench_amd import _lib
+        _lib.check(env._L.ogbx_maze_set_envs_per_wave(env._h, int(os.environ['OGBX_EPW'])))
     task = (torch.arange(base, base + n, dtype=torch.int32, device=dev) % 5) + 1
     env.reset(seed=0, options=dict(task_id=task))
     gen = torch.Generator(device=dev)

@@ -70,7 +70,12 @@ __device__ inline int64_t sample_goal(int64_t idx, int64_t final_idx, const Goal
 // end is q period + period_end -- no index load at all.  The IEEE quotient is
 // off by at most one near an integer; the remainder test corrects it.
 __device__ inline int64_t periodic_row(const ogbx_gc_buffer& buf, int64_t pick, int64_t* q_out) {
-  int64_t q = (int64_t)((double)pick / (double)buf.period_picks);
+  // the quotient estimate by the reciprocal (a function of the kernel
+  // arguments alone, so it is computed off the sample's chain): within one of
+  // floor(pick / period_picks) like the IEEE quotient, and the remainder test
+  // below makes q exact either way
+  const double inv_pp = 1.0 / (double)buf.period_picks;
+  int64_t q = (int64_t)((double)pick * inv_pp);
   int64_t r = pick - q * buf.period_picks;
   if (r < 0) {
     --q;
@@ -628,8 +633,40 @@ struct HgcPick {
   int64_t w[9];  // offsets, hv steps, hv mask, hv reward, lv steps, lv mask, lv reward, mask, reward (f64 as bits)
 };
 
+// The HGC reward tables held in the first wave's registers: lane t holds
+// entries t and t + 64 of the value / low tables (loaded at kernel start, off
+// the chain), so the chain's lookups are lane reads instead of dependent
+// global loads.  Valid when both tables have at most 128 entries (subgoal
+// steps <= 127); the mask tables are 1 - (s < K), computed in line.
+struct HgcTables {
+  double hv0, hv1, lv0, lv1;
+  bool regs;
+};
+
+__device__ __forceinline__ HgcTables hgc_tables_load(const ogbx_hgc_config& hc) {
+  HgcTables tb{0.0, 0.0, 0.0, 0.0, hc.value_subgoal_steps < 128 && hc.low_subgoal_steps < 128};
+  const int t = (int)(threadIdx.x & 63);
+  if (tb.regs) {
+    if (t <= hc.value_subgoal_steps) tb.hv0 = hc.hv_reward_table[t];
+    if (t + 64 <= hc.value_subgoal_steps) tb.hv1 = hc.hv_reward_table[t + 64];
+    if (t <= hc.low_subgoal_steps) tb.lv0 = hc.lv_reward_table[t];
+    if (t + 64 <= hc.low_subgoal_steps) tb.lv1 = hc.lv_reward_table[t + 64];
+  }
+  return tb;
+}
+
+// entry s (wave-uniform) of a register-held table
+__device__ __forceinline__ double table_lane(double v0, double v1, int64_t s) {
+  const int i = __builtin_amdgcn_readfirstlane((int)s);
+  const double v = i < 64 ? v0 : v1;
+  const int l = i & 63;
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
 __device__ inline HgcPick hgc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_config& cfg, const ogbx_hgc_config& hc,
-                                    const u32x4* wv, double v_log_q, double a_log_q, double l_log_q) {
+                                    const u32x4* wv, double v_log_q, double a_log_q, double l_log_q,
+                                    const HgcTables& tb) {
   const u32x4 w0 = wv[0], w1 = wv[1], w2 = wv[2], w3 = wv[3], w4 = wv[4];
   const int64_t npick = buf.valid_idxs ? buf.num_valid : buf.num_rows;
   const int64_t pick = (int64_t)bounded64(w0.x, w0.y, (uint64_t)npick);
@@ -690,13 +727,22 @@ __device__ inline HgcPick hgc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_con
   const double neg = cfg.gc_negative ? 1.0 : 0.0;
   p.w[0] = hvg - idx;
   p.w[1] = hv_steps;
-  p.w[2] = __double_as_longlong(hc.hv_mask_table[hv_steps]);
-  p.w[3] = __double_as_longlong(hc.hv_reward_table[hv_steps]);
+  if (tb.regs) {
+    // the tables' masks are 1 - (s < K) (datasets.py:535, 552)
+    p.w[2] = __double_as_longlong(hv_steps < hc.value_subgoal_steps ? 0.0 : 1.0);
+    p.w[3] = __double_as_longlong(table_lane(tb.hv0, tb.hv1, hv_steps));
+  } else {
+    p.w[2] = __double_as_longlong(hc.hv_mask_table[hv_steps]);
+    p.w[3] = __double_as_longlong(hc.hv_reward_table[hv_steps]);
+  }
   p.w[4] = lv_steps;
   if (hc.has_low_value_goals) {
     const double ls = idx == lvg ? 1.0 : 0.0;
     p.w[5] = __double_as_longlong(1.0 - ls);
     p.w[6] = __double_as_longlong(ls - neg);
+  } else if (tb.regs) {
+    p.w[5] = __double_as_longlong(lv_steps < hc.low_subgoal_steps ? 0.0 : 1.0);
+    p.w[6] = __double_as_longlong(table_lane(tb.lv0, tb.lv1, lv_steps));
   } else {
     p.w[5] = __double_as_longlong(hc.lv_mask_table[lv_steps]);
     p.w[6] = __double_as_longlong(hc.lv_reward_table[lv_steps]);
@@ -709,7 +755,8 @@ __device__ inline HgcPick hgc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_con
 
 __device__ inline HgcPick hgc_wave_chain(const ogbx_gc_buffer& buf, const ogbx_gc_config& cfg,
                                          const ogbx_hgc_config& hc, int64_t s, uint32_t lo, uint32_t hi, uint32_t k0,
-                                         uint32_t k1, double v_log_q, double a_log_q, double l_log_q) {
+                                         uint32_t k1, double v_log_q, double a_log_q, double l_log_q,
+                                         const HgcTables& tb) {
   const uint64_t su = (uint64_t)s;
   const uint32_t calls = hc.has_low_value_goals ? 7u : 5u;
   const uint32_t q = (uint32_t)(threadIdx.x & 63) % calls;
@@ -719,7 +766,7 @@ __device__ inline HgcPick hgc_wave_chain(const ogbx_gc_buffer& buf, const ogbx_g
   for (int c = 0; c < 7; ++c)
     ws[c] = u32x4{(uint32_t)__builtin_amdgcn_readlane((int)w.x, c), (uint32_t)__builtin_amdgcn_readlane((int)w.y, c),
                   (uint32_t)__builtin_amdgcn_readlane((int)w.z, c), (uint32_t)__builtin_amdgcn_readlane((int)w.w, c)};
-  return hgc_chain(buf, cfg, hc, ws, v_log_q, a_log_q, l_log_q);
+  return hgc_chain(buf, cfg, hc, ws, v_log_q, a_log_q, l_log_q, tb);
 }
 
 constexpr int kHgcAheadWords = OGBX_HGC_AHEAD_WORDS;
@@ -754,6 +801,10 @@ __global__ void __launch_bounds__(256) hgc_ahead_kernel(
     if (k == 3 && o.high_actor_goal_idxs) o.high_actor_goal_idxs[s] = v;
     if (k == 6 && o.low_value_goal_idxs) o.low_value_goal_idxs[s] = v;
   };
+  // the reward tables, for the first wave's chain(s); issued before anything
+  // else so that they arrive while the chain runs
+  HgcTables tb{};
+  if (t < 64 && (ahead_out || !ahead_in)) tb = hgc_tables_load(hc);
   if (ahead_in) {
     if (t < kHgcSel + 9) {
       const int64_t v = ahead_in[s * kHgcAheadWords + t];
@@ -765,7 +816,7 @@ __global__ void __launch_bounds__(256) hgc_ahead_kernel(
       }
     }
   } else if (t < 64) {
-    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, call_lo, call_hi, k0, k1, v_log_q, a_log_q, l_log_q);
+    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, call_lo, call_hi, k0, k1, v_log_q, a_log_q, l_log_q, tb);
     if (t == 0) {
 #pragma unroll
       for (int k = 0; k < kHgcSel; ++k) {
@@ -778,7 +829,7 @@ __global__ void __launch_bounds__(256) hgc_ahead_kernel(
   }
   __syncthreads();
   if (ahead_out && t < 64) {
-    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, next_lo, next_hi, k0, k1, v_log_q, a_log_q, l_log_q);
+    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, next_lo, next_hi, k0, k1, v_log_q, a_log_q, l_log_q, tb);
     if (t == 0) {
       int64_t* r = ahead_out + s * kHgcAheadWords;
 #pragma unroll

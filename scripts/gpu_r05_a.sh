@@ -22,3 +22,4 @@ done
 bash scripts/gpu_r05_floor.sh
 [ "${AB:-1}" = 1 ] || exit 0
 ROUNDS=${ROUNDS:-2} bash scripts/gpu_maze_ab.sh
+bash scripts/gpu_maze_epw.sh

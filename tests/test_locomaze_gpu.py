@@ -419,3 +419,36 @@ def test_state_restore_into_other_handle_carries_seed(gpu):
         ob, rb, _, trb, _ = b.step(acts[t])
         assert torch.equal(oa, ob) and torch.equal(tra, trb), t
     assert torch.equal(a.cur_goal_xy, b.cur_goal_xy)
+
+
+def test_results_do_not_depend_on_envs_per_wave(gpu):
+    """ogbx_maze_set_envs_per_wave (16 / 32 / 64 envs per 64-lane wave, the
+    layout knob for small per-GPU shares) changes which envs share a
+    wavefront, never an env's result: near-wall states stepped with auto-reset
+    through env.step and through K fused steps agree bit for bit across the
+    three layouts (the contact path decides everything per lane)."""
+    from ogbench_amd import _lib
+
+    rng = np.random.RandomState(17)
+    mp, _ = orc.tables('large')
+    free_cells = np.argwhere(mp == 0)
+    n, K = 3000, 12
+    c = free_cells[rng.randint(len(free_cells), size=n)]
+    q = np.stack([c[:, 1] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n), c[:, 0] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n)], 1)
+    acts = torch.tensor(rng.uniform(-1, 1, (K, n, 2)).astype(np.float32)).to(gpu)
+    res = {}
+    for epw in (64, 32, 16):
+        env = _env(gpu, n, max_episode_steps=9, auto_reset=True)
+        _lib.check(env._L.ogbx_maze_set_envs_per_wave(env._h, epw))
+        env.reset(seed=5)
+        sd = env.state_dict()
+        sd['qpos'] = torch.tensor(q, dtype=torch.float64)
+        env.load_state_dict(sd)
+        rows = []
+        for t in range(K):
+            ob, rew, term, trunc, info = env.step(acts[t])
+            rows.append(torch.cat([ob.flatten(), rew.double(), term.double(), info['success'].double()]).cpu())
+        roll = env.rollout(acts)
+        rows.append(torch.cat([roll[k].double().flatten().cpu() for k in ('obs', 'reward', 'terminated', 'success')]))
+        res[epw] = torch.cat(rows)
+    assert torch.equal(res[64], res[32]) and torch.equal(res[64], res[16])
