@@ -508,17 +508,10 @@ constexpr double kImpDelta = kPointModel.imp_dmax - kPointModel.imp_dmin;
 __device__ __forceinline__ double band_u(const PointModel& pm, double d) {
   const double x = fmin(fmax(fabs(d) * pm.inv_width, 0.0), 1.0);
   const double m = fmin(fmax(fma(2.0, x, -1.0), 0.0), 1.0);
-#ifdef OGBX_BAND_NO_OMOD
+  // (2 - 2x^2 as (1 - x^2) times 2 by the VOP3 output modifier was tried in
+  // round 5: gfx950 does not apply omod to this f64 fma -- the contact pin
+  // caught a 4.5e-5 error)
   return fma(m, m, fma(-(x + x), x, 2.0));
-#else
-  // 2 - 2x^2 as (1 - x^2) times 2 by the VOP3 output modifier: one
-  // instruction instead of an add and an fma, the same value (a power-of-two
-  // scale commutes with rounding; 1 - x^2 in [0, 1] is never subnormal
-  // unless zero)
-  double t;
-  asm("v_fma_f64 %0, %1, -%1, 1.0 mul:2" : "=v"(t) : "v"(x));
-  return fma(m, m, t);
-#endif
 }
 
 #ifdef OGBX_WAVE_STAMPS
