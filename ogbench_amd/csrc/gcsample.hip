@@ -634,9 +634,9 @@ struct HgcPick {
 };
 
 // The HGC reward tables held in the first wave's registers: lane t holds
-// entries t and t + 64 of the value / low tables (loaded at kernel start, off
-// the chain), so the chain's lookups are lane reads instead of dependent
-// global loads.  Valid when both tables have at most 128 entries (subgoal
+// entries t and t + 64 of the value / low tables (loaded when the chain
+// starts, so they arrive while it runs), and the chain's lookups are lane
+// reads instead of global loads that wait for the subgoal step counts.  Valid when both tables have at most 128 entries (subgoal
 // steps <= 127); the mask tables are 1 - (s < K), computed in line.
 struct HgcTables {
   double hv0, hv1, lv0, lv1;
@@ -646,12 +646,14 @@ struct HgcTables {
 __device__ __forceinline__ HgcTables hgc_tables_load(const ogbx_hgc_config& hc) {
   HgcTables tb{0.0, 0.0, 0.0, 0.0, hc.value_subgoal_steps < 128 && hc.low_subgoal_steps < 128};
   const int t = (int)(threadIdx.x & 63);
-  if (tb.regs) {
-    if (t <= hc.value_subgoal_steps) tb.hv0 = hc.hv_reward_table[t];
-    if (t + 64 <= hc.value_subgoal_steps) tb.hv1 = hc.hv_reward_table[t + 64];
-    if (t <= hc.low_subgoal_steps) tb.lv0 = hc.lv_reward_table[t];
-    if (t + 64 <= hc.low_subgoal_steps) tb.lv1 = hc.lv_reward_table[t + 64];
-  }
+  // clamped indices, every lane, no branch (a region around the loads made
+  // the compiler wait for them at its end); entries past K are never looked
+  // up, and with K >= 128 the lookups read the tables in memory instead
+  const int64_t kv = hc.value_subgoal_steps, kl = hc.low_subgoal_steps;
+  tb.hv0 = hc.hv_reward_table[min((int64_t)t, kv)];
+  tb.hv1 = hc.hv_reward_table[min((int64_t)t + 64, kv)];
+  tb.lv0 = hc.lv_reward_table[min((int64_t)t, kl)];
+  tb.lv1 = hc.lv_reward_table[min((int64_t)t + 64, kl)];
   return tb;
 }
 
@@ -755,8 +757,10 @@ __device__ inline HgcPick hgc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_con
 
 __device__ inline HgcPick hgc_wave_chain(const ogbx_gc_buffer& buf, const ogbx_gc_config& cfg,
                                          const ogbx_hgc_config& hc, int64_t s, uint32_t lo, uint32_t hi, uint32_t k0,
-                                         uint32_t k1, double v_log_q, double a_log_q, double l_log_q,
-                                         const HgcTables& tb) {
+                                         uint32_t k1, double v_log_q, double a_log_q, double l_log_q) {
+  // the reward tables: issued first, they arrive while the Philox calls and
+  // the goal chain run (their lookups come last)
+  const HgcTables tb = hgc_tables_load(hc);
   const uint64_t su = (uint64_t)s;
   const uint32_t calls = hc.has_low_value_goals ? 7u : 5u;
   const uint32_t q = (uint32_t)(threadIdx.x & 63) % calls;
@@ -801,10 +805,6 @@ __global__ void __launch_bounds__(256) hgc_ahead_kernel(
     if (k == 3 && o.high_actor_goal_idxs) o.high_actor_goal_idxs[s] = v;
     if (k == 6 && o.low_value_goal_idxs) o.low_value_goal_idxs[s] = v;
   };
-  // the reward tables, for the first wave's chain(s); issued before anything
-  // else so that they arrive while the chain runs
-  HgcTables tb{};
-  if (t < 64 && (ahead_out || !ahead_in)) tb = hgc_tables_load(hc);
   if (ahead_in) {
     if (t < kHgcSel + 9) {
       const int64_t v = ahead_in[s * kHgcAheadWords + t];
@@ -816,7 +816,7 @@ __global__ void __launch_bounds__(256) hgc_ahead_kernel(
       }
     }
   } else if (t < 64) {
-    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, call_lo, call_hi, k0, k1, v_log_q, a_log_q, l_log_q, tb);
+    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, call_lo, call_hi, k0, k1, v_log_q, a_log_q, l_log_q);
     if (t == 0) {
 #pragma unroll
       for (int k = 0; k < kHgcSel; ++k) {
@@ -829,7 +829,7 @@ __global__ void __launch_bounds__(256) hgc_ahead_kernel(
   }
   __syncthreads();
   if (ahead_out && t < 64) {
-    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, next_lo, next_hi, k0, k1, v_log_q, a_log_q, l_log_q, tb);
+    const HgcPick p = hgc_wave_chain(buf, cfg, hc, s, next_lo, next_hi, k0, k1, v_log_q, a_log_q, l_log_q);
     if (t == 0) {
       int64_t* r = ahead_out + s * kHgcAheadWords;
 #pragma unroll

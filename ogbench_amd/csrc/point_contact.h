@@ -573,14 +573,21 @@ __device__ __forceinline__ void local_piece_min(const LocalSlots& c, const Piece
   *uy = (h00 * r1 - h01 * r0) * idet;
 }
 
+// The corner slot's residual pair (a = n.u + kp, b = t.u) at U: one
+// definition for the mask and the settled test, so both see the same values.
+__device__ __forceinline__ void local_corner_res(const LocalSlots& c, double ux, double uy, double* a, double* b) {
+#pragma clang fp contract(fast)
+  *a = c.nx2 * ux + (c.ny2 * uy + c.kp2);
+  *b = c.nx2 * uy - c.ny2 * ux;
+}
+
 // Active-edge mask at U (local role layout, bits as edge_mask).
 __device__ __forceinline__ uint32_t local_edge_mask(const LocalSlots& c, double ux, double uy) {
-#pragma clang fp contract(fast)
   const double P = ux + uy, Q = ux - uy;
   uint32_t m = (c.kp0 < P ? 1u : 0u) | (c.kp0 < Q ? 2u : 0u) | (c.kp0 < ux ? 4u : 0u);
   m |= (c.kp1 < -Q ? 8u : 0u) | (c.kp1 < P ? 16u : 0u) | (c.kp1 < uy ? 32u : 0u);
-  const double a = c.nx2 * ux + (c.ny2 * uy + c.kp2);
-  const double b = c.nx2 * uy - c.ny2 * ux;
+  double a, b;
+  local_corner_res(c, ux, uy, &a, &b);
   m |= (a < -b ? 64u : 0u) | (a < b ? 128u : 0u) | (a < 0.0 ? 256u : 0u);
   return m;
 }
@@ -704,6 +711,9 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
       local_piece_min(c, pw, vsx, vsy, &ux, &uy);
       A2 = local_edge_mask(c, ux, uy);
     }
+    // (round 5: the test as signs of the nine residual differences against
+    // per-edge expected sign words, v_bitop3-merged -- 5 fewer instructions
+    // per stage, no vcc hazards -- measured 11.55 -> 12.2 us per launch)
     bool done = A2 == act;
     LocalSlots cn;
     if (more) local_slots(pm, k, cn);
@@ -717,28 +727,14 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
 #endif
     if (__builtin_expect(__any(!done), 0)) {
       OGBX_WPATH(0);
-#ifdef OGBX_ITER_PER_LANE
-#pragma unroll 1
-      for (int it = 0; it < kLeanIters && !done; ++it) {
-        OGBX_WPATH(20);
-#ifdef OGBX_PHYS_STATS
-        OGBX_STAT(4);
-        ++trips;
-#endif
-        act = A2;
-        piece_weights(act, pw);
-        local_piece_min(c, pw, vsx, vsy, &ux, &uy);
-        A2 = local_edge_mask(c, ux, uy);
-        done = A2 == act;
-      }
-#else
       // Every lane runs the iteration (a wave-uniform loop): typically one or
       // two lanes of the wave flip an edge, and gfx950 issues a dependent
       // chain about twice as slowly with <= 8 active lanes, so
-      // the divergent per-lane loop ran at half speed.  A settled lane is at
-      // a fixed point (act == A2, pw = piece_weights(act)): its rerun
-      // recomputes the same ux, uy and A2 bit for bit, so every lane's result
-      // equals the per-lane loop's.
+      // the divergent per-lane loop ran at half speed (round 5 A/B: 12.10 ->
+      // 11.54 us per launch at N = 65,536, 10.79 -> 10.40 at 8,192).  A
+      // settled lane is at a fixed point (act == A2, pw = piece_weights(act)):
+      // its rerun recomputes the same ux, uy and A2 bit for bit, so every
+      // lane's result equals the per-lane loop's.
 #pragma unroll 1
       for (int it = 0; it < kLeanIters; ++it) {
         OGBX_WPATH(20);
@@ -753,7 +749,6 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
         done = A2 == act;
         if (!__any(!done)) break;
       }
-#endif
       bl |= !done;
 #ifdef OGBX_PHYS_STATS
       if (trips == 1) OGBX_STAT(5);

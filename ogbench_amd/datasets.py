@@ -20,6 +20,7 @@ injected bit-exactly through ``draws=`` for parity tests.
 from __future__ import annotations
 
 import ctypes
+import operator
 import weakref
 
 import numpy as np
@@ -31,6 +32,9 @@ def _torch():
     import torch
 
     return torch
+
+
+_VERSION = operator.attrgetter('_version')
 
 
 class GcColumn(ctypes.Structure):
@@ -308,6 +312,7 @@ class GCDataset:
         self._valid = valid
         self._plain = _plain
         self._record, self._rec_off, self._rec_stride, self._rec_src = self._row_record(dataset)
+        self._rec_index()
 
         def thresh(p_traj, p_cur):
             return p_traj / (1.0 - p_cur) if p_cur != 1.0 else 0.0  # datasets.py:321
@@ -385,6 +390,11 @@ class GCDataset:
         replaced since it was built (same layout, same record buffer: the
         cached column descriptors stay valid, except on replacement)."""
         ds = self.dataset
+        # fast check (every sample() call): the packed columns are the same
+        # tensor objects with the same version counters
+        if (all(map(operator.is_, map(ds.get, self._rec_keys), self._rec_tensors))
+                and tuple(map(_VERSION, self._rec_tensors)) == self._rec_versions):
+            return
         stale = False
         for k, t, _, _, ver in self._rec_src:
             cur = ds.get(k)
@@ -399,6 +409,12 @@ class GCDataset:
             src = tuple((k, ds[k], o, rb) for k, _, o, rb, _ in self._rec_src)
             self._fill_record(self._record, src)
             self._rec_src = tuple((k, t, o, rb, t._version) for k, t, o, rb in src)
+            self._rec_index()
+
+    def _rec_index(self):
+        self._rec_keys = tuple(e[0] for e in self._rec_src)
+        self._rec_tensors = tuple(e[1] for e in self._rec_src)
+        self._rec_versions = tuple(e[4] for e in self._rec_src)
 
     def _column(self, src_key, dst, select):
         """Descriptor of one gathered column (from the row record when the key

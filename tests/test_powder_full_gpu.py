@@ -370,7 +370,7 @@ def test_kept_pointer_write_and_read_only_views(gpu):
     through its kept pointer steps bit-identically to one restored with
     load_state_dict, and world_ids / world_full read every step leave the
     observations unchanged."""
-    n, K, T = 8, 24, 10
+    n, K, T = 8, 24, 11
     a, c, d = (_env(gpu, n, ne=5, size=64, max_episode_steps=50, auto_reset=True) for _ in range(3))
     opts = dict(task_id=torch.arange(n, device=gpu) % 5 + 1)
     a.reset(seed=3, options=opts)
