@@ -123,6 +123,20 @@ def _per_launch_ms(fn, launches, dev, host_us=120.0):
     return a.elapsed_time(b) / launches
 
 
+def _host_us_per_call(fn, calls, dev):
+    """Host time of one call of `fn` (Python + ctypes + the HIP launch) with
+    the device held by a spin kernel, so that no call waits on the GPU: the
+    host-side bound on the call rate, reported beside the device time."""
+    torch.cuda.synchronize(dev)
+    torch.cuda._sleep(int(calls * 60e-6 * 2.4e9))
+    t0 = time.perf_counter()
+    for i in range(calls):
+        fn(i)
+    dt = time.perf_counter() - t0
+    torch.cuda.synchronize(dev)
+    return dt / calls * 1e6
+
+
 def _median_launch_ms(fn, launches, dev, host_us=60.0):
     """Median of per-launch HIP event pairs on the launch stream (torch's
     current stream, which libogbx launches on) around each of `launches`
@@ -206,7 +220,7 @@ def bench_pointmaze(args, world, rank, dev):
     alg_bytes = 87 * n  # 87 B per env-step
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
-    extra = {}
+    extra = {'host_us_per_step': _host_us_per_call(step, 500, dev)}
     if args.no_extras:
         return _finish_pointmaze(args, world, rank, total, n, value, ms_per_step, kern_ms, alg_bytes, achieved,
                                  extra, env, kern_info)
@@ -516,7 +530,7 @@ def bench_gcsample(args, world, rank, dev):
     def fused(i):
         gc.sample(B, num_batches=NB)
 
-    extra = {}
+    extra = {'host_us_per_call': _host_us_per_call(step, 500, dev)}
     if not args.no_extras:
         fdt0 = _timed(step_fresh, args.steps, world, dev)
         extra['fresh_alloc_samples_per_s'] = B * args.steps * world / fdt0
@@ -584,7 +598,7 @@ def bench_hgcsample(args, world, rank, dev):
     # read and written, + valid_idxs/traj_end lookups 16 + 9 x 8-B scalars written
     per_sample = 2 * (12 * 276 + 84 + 8) + 16 + 72
     achieved = per_sample * B / (kern_ms * 1e-3) / 1e9
-    extra = {}
+    extra = {'host_us_per_call': _host_us_per_call(step, 500, dev)}
     if not args.no_extras:
         NB = 128
         big = hgc.sample(B, num_batches=NB)
@@ -595,7 +609,7 @@ def bench_hgcsample(args, world, rank, dev):
         reps = max(1, args.steps // 32)
         fdt = _timed(fused, reps, world, dev)
         fk_ms = _per_launch_ms(fused, 5, dev)
-        extra = dict(fused_128x1024_samples_per_s=B * NB * reps * world / fdt, fused_128x1024_kernel_ms=fk_ms,
+        extra.update(fused_128x1024_samples_per_s=B * NB * reps * world / fdt, fused_128x1024_kernel_ms=fk_ms,
                      fused_128x1024_achieved_GBs=per_sample * B * NB / (fk_ms * 1e-3) / 1e9)
     result = dict(
         metric='HGCDataset.sample samples/sec, humanoidmaze-large-navigate-v0 1M-row buffer, batch 1024',

@@ -12,7 +12,9 @@ F="-O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wno-unused-func
 mkdir -p build/var
 SRC=${SRC:-locomaze}
 scripts/check_macros.sh ogbench_amd/csrc/$SRC.hip "$@"
-$H $F "$@" -c ogbench_amd/csrc/$SRC.hip -o build/var/${SRC}_$name.o
+# the Makefile's per-file flags (FLAGS_<src>), then the variant's
+PF=$(make -s -C ogbench_amd/csrc -p 2>/dev/null | sed -n "s/^FLAGS_$SRC := //p")
+$H $F $PF "$@" -c ogbench_amd/csrc/$SRC.hip -o build/var/${SRC}_$name.o
 objs=$(ls build/obj/*.o | grep -v "/$SRC\.o" | tr '\n' ' ')
 mkdir -p _abx
 $H --offload-arch=gfx950 -shared -fPIC -o _abx/libogbx_$name.so $objs build/var/${SRC}_$name.o

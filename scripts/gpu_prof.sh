@@ -18,6 +18,7 @@ ARGS="--workload $WL --steps $STEPS --warmup ${WARMUP:-100} --no-cpu-baseline --
 TAG=${TAG:-$WL}
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
   python3 bench.py $ARGS > gpurun_out/prof_${TAG}.log 2>&1 || exit $?
+[ "${PMC:-1}" = 1 ] || { tail -1 gpurun_out/prof_${TAG}.log; exit 0; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_$TAG -o run --output-format csv -- \
   python3 bench.py $ARGS > gpurun_out/pmc_fetch_${TAG}.log 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_$TAG -o run --output-format csv -- \

@@ -16,7 +16,7 @@ import json, sys
 r = json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
 f = r['roofline']
 print(f"{r['config']['workload']}: {r['value']/1e6:.1f} M/s, {r['ms_per_step']*1e3:.2f} us/step, {f['kernel']} "
-      f"timed {f['kernel_ms_timed_region']*1e3:.2f} b2b {f['kernel_ms_back_to_back']*1e3:.2f} us")
+      f"timed {f['kernel_ms_timed_region']*1e3:.2f} b2b {f['kernel_ms_back_to_back']*1e3:.2f} us host {r['extra'].get('host_us_per_call', 0):.2f} us")
 PY
 done
 ROUNDS=${ROUNDS:-2} bash scripts/gpu_maze_ab.sh
