@@ -1,7 +1,11 @@
 """Diagnostic: physics-kernel time on the bench's stationary states, all envs
-vs the contact envs only (compacted), with HIP events.  If the compacted launch
-(~1/5 of the envs, ~1/5 of the waves) takes as long as the full one, the
-kernel is bound by one wave's contact chain, not by the number of waves."""
+vs the contact envs only (compacted) vs the free envs only, with HIP events
+around launches queued behind a spin kernel (device-paced: env.physics()
+allocates its outputs, so a host-paced loop measures the host).  If the
+compacted launch (~1/12 of the envs and waves) takes as long as the full one,
+the kernel is bound by one wave's contact chain, not by the number of
+waves.  (Rounds 3-4 ran this host-paced: their "free only" 9.1 us was the
+Python call, not the kernel.)"""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, ogbench_amd
@@ -21,11 +25,12 @@ qc, ac = q[c].contiguous(), a[c].contiguous()
 qf, af = q[~c].contiguous(), a[~c].contiguous()
 
 
-def t(qq, aa, reps=50):
+def t(qq, aa, reps=200):
     for _ in range(5):
         env.physics(qq, aa)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
+    torch.cuda._sleep(int(reps * 60e-6 * 2.4e9))
     s.record()
     for _ in range(reps):
         env.physics(qq, aa)
