@@ -220,7 +220,7 @@ def bench_pointmaze(args, world, rank, dev):
     alg_bytes = 87 * n  # 87 B per env-step
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
-    extra = {'host_us_per_step': _host_us_per_call(step, 500, dev)}
+    extra = {'host_us_per_step': _host_us_per_call(step, 200, dev)}
     if args.no_extras:
         return _finish_pointmaze(args, world, rank, total, n, value, ms_per_step, kern_ms, alg_bytes, achieved,
                                  extra, env, kern_info)
@@ -530,7 +530,7 @@ def bench_gcsample(args, world, rank, dev):
     def fused(i):
         gc.sample(B, num_batches=NB)
 
-    extra = {'host_us_per_call': _host_us_per_call(step, 500, dev)}
+    extra = {'host_us_per_call': _host_us_per_call(step, 200, dev)}
     if not args.no_extras:
         fdt0 = _timed(step_fresh, args.steps, world, dev)
         extra['fresh_alloc_samples_per_s'] = B * args.steps * world / fdt0
@@ -598,7 +598,7 @@ def bench_hgcsample(args, world, rank, dev):
     # read and written, + valid_idxs/traj_end lookups 16 + 9 x 8-B scalars written
     per_sample = 2 * (12 * 276 + 84 + 8) + 16 + 72
     achieved = per_sample * B / (kern_ms * 1e-3) / 1e9
-    extra = {'host_us_per_call': _host_us_per_call(step, 500, dev)}
+    extra = {'host_us_per_call': _host_us_per_call(step, 200, dev)}
     if not args.no_extras:
         NB = 128
         big = hgc.sample(B, num_batches=NB)
