@@ -688,6 +688,100 @@ struct FullWorld {
     dc = (int)((0x901Au >> (2 * d)) & 3u) - 1;
   }
 
+  // Cells a velocity pass may move, listed when at most kSwapList (two
+  // chunks of a wave).
+  // (A/B, medium / hard per step: 128 161.3 / 186.0 us, 64 163.2 / 188.9,
+  // 256 162.4 / 187.3, 512 169.0 / 194.9, the block rounds alone 166.0 /
+  // 191.3: a longer list costs registers in the whole inlined forward)
+  static constexpr uint32_t kSwapList = 128;
+
+  // block_or of the bins plus the world's candidate count (cells with a bin)
+  // and this wave's first list slot, through one barrier.
+  __device__ __forceinline__ uint32_t bins_reduce(uint32_t dirs, Codes binr, uint32_t* total, uint32_t* base) const {
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+      cnt += (uint32_t)__popcll(__ballot(((uint32_t)(binr >> (8 * k)) & 0xFFu) != 0xFFu));
+    dirs = wave_or(dirs);
+    const int w = (int)(threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0) {
+      s.red_v[w] = (int32_t)dirs;
+      s.red_e[w] = (int32_t)cnt;  // red_e: errors() reads it only across its own barriers
+    }
+    sync();
+    uint32_t all = 0, tot = 0, b = 0;
+#pragma unroll
+    for (int q = 0; q < NT / 64; ++q) {
+      all |= (uint32_t)s.red_v[q];
+      const uint32_t c = (uint32_t)s.red_e[q];
+      b += q < w ? c : 0u;
+      tot += c;
+    }
+    *total = tot;
+    *base = b;
+    return all;
+  }
+
+  // The swap rounds of one velocity pass run by the first wave over the list
+  // of cells that may move (same decisions and writes as the block rounds;
+  // the list is in cell order within each wave's slice, and no two matches
+  // of a round write the same sw entry, so the order does not matter).
+  __device__ __forceinline__ void swap_rounds_listed(Codes binr, uint32_t dirs, uint32_t total, uint32_t base) const {
+    static_assert(kSwapList <= C / 2, "list of uint16 entries in f2");
+    uint16_t* list = reinterpret_cast<uint16_t*>(s.f2);
+    const int lane = (int)(threadIdx.x & 63u);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t off = base;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
+      const uint32_t b = (uint32_t)(binr >> (8 * k)) & 0xFFu;
+      const uint64_t m = __ballot(b != 0xFFu);
+      if (b != 0xFFu) list[off + (uint32_t)__popcll(m & lt)] = (uint16_t)(cell(k) | (int)(b << 12));
+      off += (uint32_t)__popcll(m);
+    }
+    sync();
+    if (threadIdx.x < 64) {
+      constexpr int kChunks = kSwapList / 64;
+#pragma unroll 1
+      for (int d = 0; d < 8; ++d) {
+        if (!((dirs >> d) & 1u)) continue;
+        int dr, dc;
+        dir_of(d, dr, dc);
+        int ii[kChunks], jj[kChunks];
+        uint32_t mk = 0;
+#pragma unroll
+        for (int q = 0; q < kChunks; ++q) {  // phase 1: f1 = d + 1 on matches
+          const uint32_t e = (uint32_t)(lane + 64 * q);
+          ii[q] = 0;
+          jj[q] = 0;
+          if (e < total) {
+            const uint32_t ent = list[e];
+            if ((ent >> 12) == (uint32_t)d) {
+              const int i = (int)(ent & 0xFFFu), r = i / W, c = i % W;
+              const int j = ((r + dr) & (H - 1)) * W + ((c + dc) & (W - 1));
+              ii[q] = i;
+              jj[q] = j;
+              if ((s.sw[i] == -1) & (s.sw[j] == -1) & (fid(s.a[j]) == kEmpty)) {
+                s.f1[i] = (uint8_t)(d + 1);
+                mk |= 1u << q;
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kChunks; ++q) {  // phase 2: the choices
+          if ((mk >> q) & 1u) {
+            const int i = ii[q], r = i / W, c = i % W;
+            const int back = ((r - dr) & (H - 1)) * W + ((c - dc) & (W - 1));
+            s.sw[jj[q]] = (int8_t)((d + 4) & 7);
+            if (s.f1[back] != (uint8_t)(d + 1)) s.sw[i] = (int8_t)d;
+          }
+        }
+      }
+    }
+    sync();
+  }
+
   __device__ __forceinline__ void velocity() const {
     fence_idx();
 #pragma unroll 1
@@ -723,7 +817,9 @@ struct FullWorld {
         s.sw[i] = -1;
         s.f1[i] = 0;
       }
-      dirs = block_or(dirs);
+      // the world's bins and its count of cells that may move (one barrier)
+      uint32_t ncand = 0, wbase = 0;
+      dirs = bins_reduce(dirs, binr, &ncand, &wbase);
       if (dirs == 0) {
         // no swap anywhere: v = v * 0.5 + v * 0.5 in place
 #pragma unroll
@@ -743,6 +839,12 @@ struct FullWorld {
       // target's choice wins when a matched cell is itself a target, as in
       // the reference's where(m, a, .) then where(opp, a + 4, .).  Rounds whose
       // bin no cell occupies are identities and skipped.
+      if (ncand <= kSwapList) {
+        // few cells may move: list them (cell | bin << 12 in f2, free during
+        // this rule) and let ONE wave run every round -- its LDS operations
+        // are ordered, so the rounds need no barriers (two per round below)
+        swap_rounds_listed(binr, dirs, ncand, wbase);
+      } else
 #pragma unroll 1
       for (int d = 0; d < 8; ++d) {
         if (!((dirs >> d) & 1u)) continue;
