@@ -73,7 +73,8 @@ __host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
 // The same Philox4x32-10 with both halves of a round's 32x32 -> 64 product
 // from one v_mad_u64_u32 (LLVM emits a v_mul_hi_u32 + v_mul_lo_u32 pair):
 // +6 % throughput with identical words (scripts/micro/philox_mul.hip).  For
-// throughput-bound callers (every lane drawing, e.g. powder rand fields);
+// throughput-bound callers (every lane drawing, e.g. powder rand fields) with
+// wave-uniform keys (k0, k1 go in scalar operands);
 // latency-bound chains keep the pair, whose halves issue independently.
 __device__ __forceinline__ u32x4 philox4x32_10_wide(u32x4 c, uint32_t k0, uint32_t k1) {
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
@@ -84,9 +85,12 @@ __device__ __forceinline__ u32x4 philox4x32_10_wide(u32x4 c, uint32_t k0, uint32
     asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p0), "=s"(c0) : "v"(M0), "v"(c.x));
     asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(p1), "=s"(c1) : "v"(M1), "v"(c.z));
     u32x4 n;
-    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    // hi ^ c ^ key as one v_bitop3_b32 (truth table 0x96: S0 ^ S1 ^ S2; gfx950
+    // has no v_xor3_b32) with the key as its scalar operand (LLVM
+    // keeps two v_xor_b32 here): callers pass wave-uniform keys
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n.x) : "v"((uint32_t)(p1 >> 32)), "v"(c.y), "s"(k0));
     n.y = (uint32_t)p1;
-    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n.z) : "v"((uint32_t)(p0 >> 32)), "v"(c.w), "s"(k1));
     n.w = (uint32_t)p0;
     c = n;
     k0 += W0;
