@@ -506,7 +506,7 @@ def bench_gcsample(args, world, rank, dev):
     if 'OGBX_GC_LOOKAHEAD' in os.environ:  # A/B knob (the sampler's lookahead config key)
         cfg['lookahead'] = os.environ['OGBX_GC_LOOKAHEAD'] != '0'
     gc = GCDataset(Dataset(data, device=dev), cfg, seed=rank)
-    gc_kernel = 'gc_ahead_kernel' if gc._lookahead else 'gc_sample_kernel'  # the launch of a steady call
+    gc_kernel = 'gc_ahead_kernel<true>' if gc._lookahead else 'gc_sample_kernel'  # the launch of a steady call
     B = 1024
     batch = gc.sample(B)
 
@@ -582,7 +582,7 @@ def bench_hgcsample(args, world, rank, dev):
     if 'OGBX_GC_LOOKAHEAD' in os.environ:  # A/B knob (the sampler's lookahead config key)
         cfg['lookahead'] = os.environ['OGBX_GC_LOOKAHEAD'] != '0'
     hgc = HGCDataset(Dataset(data, device=dev), cfg, seed=rank)
-    hgc_kernel = 'hgc_ahead_kernel' if hgc._lookahead else 'hgc_sample_kernel'  # the launch of a steady call
+    hgc_kernel = 'hgc_ahead_kernel<true>' if hgc._lookahead else 'hgc_sample_kernel'  # the launch of a steady call
     B = 1024
     batch = hgc.sample(B)
 

@@ -10,8 +10,8 @@ for wl in $WLS; do
     pointmaze) K=maze_step_kernel; S=2000 ;;
     powder) K=pw_step_kernel; S=600 ;;
     powder-medium|powder-hard) K=pwf_light_step_kernel+pwf_step_kernel; S=600 ;;
-    gcsample) K=gc_ahead_kernel; S=300 ;;
-    hgcsample) K=hgc_ahead_kernel; S=300 ;;
+    gcsample) K="gc_ahead_kernel<true>"; S=300 ;;
+    hgcsample) K="hgc_ahead_kernel<true>"; S=300 ;;
     antmaze) K=ant_step_kernel; S=2000 ;;
     *) echo "unknown workload $wl"; exit 2 ;;
   esac
