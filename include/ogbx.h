@@ -34,8 +34,9 @@ extern "C" {
 
 /* History: 4 = rounds 1-3; 5 adds ogbx_gc_sample_ahead, ogbx_hgc_sample_ahead,
  * ogbx_maze_set_seed, ogbx_powder_set_seed, ogbx_stream_version,
- * ogbx_powder_state_view, ogbx_powder_state_written and the sampler plans
- * ogbx_gc_plan_* (no entry point of 4 changed its signature or meaning). */
+ * ogbx_powder_state_view, ogbx_powder_state_written, ogbx_powder_set_phase
+ * and the sampler plans ogbx_gc_plan_* (no entry point of 4 changed its
+ * signature or meaning). */
 #define OGBX_ABI_VERSION 5
 
 typedef enum {
@@ -629,6 +630,16 @@ ogbx_status ogbx_powder_state_view(ogbx_powder_t env, const uint8_t** world, con
  * the write comes after a step that followed the pointer's hand-out (a host
  * that keeps the pointers); harmless otherwise. */
 ogbx_status ogbx_powder_state_written(ogbx_powder_t env);
+
+/* Phase hint (medium/hard): every env steps in phase, `phase` steps after a
+ * common all-env reset (what an unmasked ogbx_powder_reset sets to 0); -1 =
+ * unknown (what ogbx_powder_state_written and masked resets set).  With it
+ * the host skips the light kernel on steps where every in-phase env needs the
+ * full kernel, and launches the full kernel in its sparse form (a few envs
+ * per workgroup) on render-only steps.  A wrong hint only costs time: envs out
+ * of the phase are stepped bit-identically either way.  For a host restoring
+ * a checkpoint of envs it knows to be in phase. */
+ogbx_status ogbx_powder_set_phase(ogbx_powder_t env, int64_t phase);
 
 /* The seed of the steps' Philox draws (invalid-action replacements, rand
  * fields, auto-resets), as the last ogbx_powder_reset set it; restores it with

@@ -123,6 +123,7 @@ _SIGNATURES = {
     'ogbx_powder_full_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p)]),
     'ogbx_powder_state_view': (c_int32, [c_void_p, P(c_void_p), P(c_void_p), P(c_void_p), P(c_void_p)]),
     'ogbx_powder_state_written': (c_int32, [c_void_p]),
+    'ogbx_powder_set_phase': (c_int32, [c_void_p, c_int64]),
     'ogbx_powder_forward': (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
     'ogbx_powder_forward_full': (
         c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]

@@ -256,6 +256,13 @@ class PowderworldEnv:
             g.copy_(sd['goal'])
         _lib.check(self._L.ogbx_powder_state_written(self._h))
 
+    def set_step_phase(self, phase):
+        """Declare that every env steps in phase, `phase` steps after a common
+        all-env reset (-1: unknown, what load_state_dict leaves).  Only the
+        launch plan of medium/hard steps uses it; a wrong hint costs time, not
+        results (include/ogbx.h ogbx_powder_set_phase)."""
+        _lib.check(self._L.ogbx_powder_set_phase(self._h, int(phase)))
+
     def forward(self, worlds, steps=1):
         """PWSim.forward (sim.py:363-380) on packed worlds uint8 [n, H, W]."""
         torch = _torch()

@@ -66,10 +66,14 @@ def main():
     parts = a.kernel.split('+')
     per = []
     for k in parts:
-        avg, n = 0.0, 0
+        # every row whose name contains the part (template instances of one
+        # kernel, e.g. the powder step kernel's dense and sparse forms)
+        tot, n = 0.0, 0
         for row in rows:
             if k in row['Name']:
-                avg, n = float(row['AverageNs']), int(row['Calls'])
+                tot += float(row['TotalDurationNs'])
+                n += int(row['Calls'])
+        avg = tot / n if n else 0.0
         fk, nfk = counter_avg(os.path.join(a.out, f'pmc_fetch_{a.workload}'), 'FETCH_SIZE', k)
         wk, nwk = counter_avg(os.path.join(a.out, f'pmc_write_{a.workload}'), 'WRITE_SIZE', k)
         per.append((avg, n, fk, nfk, wk, nwk))

@@ -38,7 +38,7 @@ ABI5_SYMBOLS = {
     # powderworld
     'ogbx_powder_create', 'ogbx_powder_destroy', 'ogbx_powder_describe', 'ogbx_powder_goal_worlds',
     'ogbx_powder_reset', 'ogbx_powder_step', 'ogbx_powder_state', 'ogbx_powder_state_view',
-    'ogbx_powder_state_written', 'ogbx_powder_set_seed', 'ogbx_powder_full_state', 'ogbx_powder_forward',
+    'ogbx_powder_state_written', 'ogbx_powder_set_phase', 'ogbx_powder_set_seed', 'ogbx_powder_full_state', 'ogbx_powder_forward',
     'ogbx_powder_forward_full', 'ogbx_powder_task_table',
     # offline replay
     'ogbx_gc_sample', 'ogbx_gc_sample_ahead', 'ogbx_hgc_sample', 'ogbx_hgc_sample_ahead', 'ogbx_gc_traj_end',

@@ -403,11 +403,11 @@ def test_kept_pointer_write_and_read_only_views(gpu):
 
 @pytest.mark.parametrize('ne,size', [(5, 64), (8, 32)])
 def test_out_of_phase_envs_after_full_reset_match_fused(gpu, ne, size):
-    """The host skips the light kernel on steps where every env reset together
-    needs the full kernel (ogbx_powder_env::phase).  Envs out of that phase
-    (here: a mixed-stage state loaded after an all-env reset, so the host's
-    guess is wrong for some envs on every step) must still step bit-for-bit as
-    the fused rollout from the same state."""
+    """A mixed-stage state loaded after an all-env reset: load_state_dict drops
+    the host's phase guess (ogbx_powder_env::phase), so every step launches the
+    light kernel and the one-env full kernel; the steps must match the fused
+    rollout from the same state bit for bit (a wrong guess:
+    test_wrong_phase_hint_matches_fused)."""
     n, K = 9, 16
     src = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
     src.reset(seed=4, options=dict(task_id=torch.arange(n, device=gpu) % 5 + 1))
@@ -425,6 +425,45 @@ def test_out_of_phase_envs_after_full_reset_match_fused(gpu, ne, size):
     a.load_state_dict(sd)                       # ... but the envs are not in that phase
     b.reset(seed=4, options=dict(task_id=1))
     b.load_state_dict(sd)
+    acts = rng.randint(0, hi, size=(K, n))
+    out = b.rollout(acts)
+    for t in range(K):
+        ob, rew, term, trunc, info = a.step(acts[t])
+        assert torch.equal(out['obs'][t], ob), t
+        assert torch.equal(out['reward'][t], rew), t
+        assert torch.equal(out['truncated'][t].bool(), trunc), t
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in ('world', 'ctrl', 'elapsed', 'episode', 'momentum', 'velocity', 'goal'):
+        assert torch.equal(sa[k], sb[k]), k
+
+
+@pytest.mark.parametrize('ne,size,phase', [(5, 64, 0), (5, 64, 1), (8, 32, 2), (8, 64, 5)])
+def test_wrong_phase_hint_matches_fused(gpu, ne, size, phase):
+    """A wrong phase hint (set_step_phase on a mixed-stage state) makes the host
+    pick the wrong launch plan on most steps: no light kernel on a step where
+    some envs are render-only (the dense full kernel steps them), and the
+    sparse full kernel (8 envs per workgroup, pwf_step_kernel<WS, true>) on
+    render-only steps where some envs need a forward or an auto-reset.  Both
+    must step bit-for-bit as the fused rollout from the same state."""
+    n, K = 19, 18
+    src = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    src.reset(seed=6, options=dict(task_id=torch.arange(n, device=gpu) % 5 + 1))
+    rng = np.random.RandomState(30 + phase)
+    hi = max(ne, src._xy_action_size) + 1
+    src.step(rng.randint(0, hi, size=n))
+    src.reset(options=dict(task_id=3), mask=torch.tensor([i % 3 != 0 for i in range(n)], dtype=torch.uint8,
+                                                           device=gpu))
+    src.step(rng.randint(0, hi, size=n))
+    src.reset(options=dict(task_id=4), mask=torch.tensor([i % 4 == 1 for i in range(n)], dtype=torch.uint8,
+                                                           device=gpu))
+    sd = src.state_dict()
+    assert len(set((sd['ctrl'] & 3).tolist())) == 3
+    a = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    b = _env(gpu, n, ne=ne, size=size, max_episode_steps=7, auto_reset=True)
+    for x in (a, b):
+        x.reset(seed=6, options=dict(task_id=1))
+        x.load_state_dict(sd)
+    a.set_step_phase(phase)
     acts = rng.randint(0, hi, size=(K, n))
     out = b.rollout(acts)
     for t in range(K):
