@@ -9,7 +9,7 @@ LIBS=${LIBS:-"ogbench_amd/libogbx.so $(ls _abx/libogbx_*.so 2>/dev/null | tr '\n
 for r in $(seq 1 ${ROUNDS:-2}); do
   for lib in $LIBS; do
     for wl in ${WLS:-gcsample hgcsample}; do
-      OGBX_LIB=$PWD/$lib timeout -k 10 200 python bench.py --workload $wl --steps ${STEPS:-2000} --warmup 100 --no-extras \
+      OGBX_LIB=$PWD/$lib timeout -k 10 200 python bench.py --workload $wl --steps ${STEPS:-2000} --warmup 100 --no-extras ${EXTRA:-} \
         --no-cpu-baseline > gpurun_out/ab.log 2>&1 || { tail -20 gpurun_out/ab.log; exit 4; }
       python - gpurun_out/ab.log "$lib" "$wl" <<'PY'
 import json, sys
