@@ -166,7 +166,10 @@ __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, 
 // Otherwise each column is copied with its widest aligned unit.
 // Waves [wave0, blockDim.x / 64) copy (wave0 = 1: the first wave computes the
 // next call's selectors meanwhile, gc_ahead_kernel).
-template <int kSel>
+// kNt: non-temporal stores on the small-tile path (the HGC hit kernel: its 3.6
+// MB of rows per launch leave less to the end-of-kernel write-back, 6.44 ->
+// 6.34 us; GC's 1.3 MB measured 4.34 -> 4.38 us and keeps plain stores)
+template <int kSel, bool kNt = false>
 __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int64_t (*sel)[kGcMaxTile], int64_t base,
                                  int n_here, bool flat4, int wave0 = 0) {
   if ((int)(threadIdx.x >> 6) < wave0) return;
@@ -204,7 +207,12 @@ __device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int6
       for (int u = 0; u < kJ; ++u)
 #pragma unroll
         for (int q = 0; q < kSlots; ++q)
-          if (d[u][q]) *d[u][q] = v[u][q];
+          if (d[u][q]) {
+            if constexpr (kNt)
+              __builtin_nontemporal_store(v[u][q], d[u][q]);
+            else
+              *d[u][q] = v[u][q];
+          }
     }
     return;
   }
@@ -852,7 +860,7 @@ __global__ void __launch_bounds__(256) hgc_ahead_kernel(
     }
     if (lane < kHgcSel) sel[lane][wave] = ahead_in[s * kHgcAheadWords + lane];
     __builtin_amdgcn_wave_barrier();
-    copy_tile<0>(cols, num_cols, reinterpret_cast<const int64_t(*)[kGcMaxTile]>(&sel[0][wave]), s, 1, flat4, 1);
+    copy_tile<0, true>(cols, num_cols, reinterpret_cast<const int64_t(*)[kGcMaxTile]>(&sel[0][wave]), s, 1, flat4, 1);
     return;
   }
   if (t < 64) {
