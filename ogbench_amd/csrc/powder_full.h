@@ -122,7 +122,22 @@ __device__ unsigned long long g_pwf_rule[4096 * 16];
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_pwf_rule[blockIdx.x * 16 + (slot)] += _t - _rs_prev; \
     _rs_prev = _t;                                                                            \
   } while (0)
+// sub-stamps inside one rule (slots 10..14; the velocity rule's parts)
+#define OGBX_VS_BEGIN() unsigned long long _vs_prev = __builtin_amdgcn_s_memtime()
+#define OGBX_VS(slot) OGBX_RS_AT(_vs_prev, slot)
+#define OGBX_RS_AT(prev, slot)                                                                \
+  do {                                                                                        \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                               \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_pwf_rule[blockIdx.x * 16 + (slot)] += _t - (prev); \
+    (prev) = _t;                                                                              \
+  } while (0)
 #else
+#define OGBX_VS_BEGIN() \
+  do {                  \
+  } while (0)
+#define OGBX_VS(slot) \
+  do {                \
+  } while (0)
 #define OGBX_RS_BEGIN() \
   do {                  \
   } while (0)
@@ -784,6 +799,7 @@ struct FullWorld {
 
   __device__ __forceinline__ void velocity() const {
     fence_idx();
+    OGBX_VS_BEGIN();
 #pragma unroll 1
     for (int pass = 0; pass < 2; ++pass) {
       fence_idx();
@@ -820,16 +836,26 @@ struct FullWorld {
       // the world's bins and its count of cells that may move (one barrier)
       uint32_t ncand = 0, wbase = 0;
       dirs = bins_reduce(dirs, binr, &ncand, &wbase);
+      OGBX_VS(10);
       if (dirs == 0) {
-        // no swap anywhere: v = v * 0.5 + v * 0.5 in place
+        // no swap anywhere: v = v * 0.5 + v * 0.5 in place.  With no cell
+        // above pass 0's threshold (|v| > 1) none is above pass 1's (|v| > 2)
+        // either -- the in-place update changes no normal float, and a
+        // subnormal component stays far below both -- so pass 1 is the same
+        // update again, applied here without its bins and barrier.
+        const int reps = pass == 0 ? 2 : 1;
 #pragma unroll
         for (int k = 0; k < CPT; ++k) {
           float2 v = s.v[cell(k)];
-          v.x = v.x * 0.5f + v.x * 0.5f;
-          v.y = v.y * 0.5f + v.y * 0.5f;
+          for (int r = 0; r < reps; ++r) {
+            v.x = v.x * 0.5f + v.x * 0.5f;
+            v.y = v.y * 0.5f + v.y * 0.5f;
+          }
           s.v[cell(k)] = v;
         }
         sync();
+        OGBX_VS(12);
+        if (pass == 0) break;
         continue;
       }
       // Swap rounds in direction order (sim.py:950-962), sparse: only the
@@ -873,6 +899,7 @@ struct FullWorld {
         }
         sync();
       }
+      OGBX_VS(11);
       Moves mvs;
 #pragma unroll
       for (int k = 0; k < CPT; ++k) {
@@ -893,6 +920,7 @@ struct FullWorld {
         v.y = v.y * 0.5f + v.y * 0.5f;
         s.v[i] = v;
       });
+      OGBX_VS(12);
     }
     // decay (x0.95) fused into the 3x3 blur (zero padded) of the decayed
     // field, NumPy's einsum summation order.  A wave holds whole rows: each
@@ -930,6 +958,7 @@ struct FullWorld {
 #pragma unroll
     for (int k = 0; k < CPT; ++k) s.v[cell(k)] = res[k];
     sync();
+    OGBX_VS(13);
   }
 
   // The value at column col - 1 / col + 1 of the same row (a wave holds whole

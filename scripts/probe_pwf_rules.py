@@ -31,6 +31,8 @@ def report(tag, d):
     print(f'{level} {tag}: {fw} forwards; cycles per forward (mean over envs): {tot / fw:.0f}')
     for k, nm in enumerate(names):
         print(f'  {nm:15s} {d[:, k].sum() / fw:8.0f} cyc  {100 * d[:, k].sum() / tot:5.1f} %')
+    for k, nm in zip(range(10, 14), ['vel: bins', 'vel: rounds', 'vel: commit', 'vel: blur']):
+        print(f'    {nm:13s} {d[:, k].sum() / fw:8.0f} cyc')
 
 
 for i in range(120):
