@@ -301,24 +301,24 @@ struct FullWorld {
     }
     sync();
   }
+  // Written in place with no barrier between the reads and the writes: a
+  // stone cell's support reads only the id bits (0-4) of its upper diagonal
+  // neighbours, and the rule writes only the GravityInter bit (5) of its own
+  // cell, so a neighbour's byte read before or after that neighbour's own
+  // update gives the same id (LDS byte stores do not tear).
   __device__ __forceinline__ void stone() const {
     fence_idx();
-    uint32_t na[CPT];
 #pragma unroll
     for (int k = 0; k < CPT; ++k) {
       const int i = cell(k);
-      uint32_t a = s.a[i];
+      const uint32_t a = s.a[i];
       if (fid(a) == kStone) {
         const int jl = zp(k, -1, -1), jr = zp(k, -1, 1);
         const uint32_t al = s.a[jl >= 0 ? jl : 0], ar = s.a[jr >= 0 ? jr : 0];
         const int sup = ((jl >= 0) & (fid(al) == kStone)) + ((jr >= 0) & (fid(ar) == kStone));
-        a = (a & ~kGrav) | (sup < 2 ? kGrav : 0u);
+        s.a[i] = (uint8_t)((a & ~kGrav) | (sup < 2 ? kGrav : 0u));
       }
-      na[k] = a;
     }
-    sync();
-#pragma unroll
-    for (int k = 0; k < CPT; ++k) s.a[cell(k)] = (uint8_t)na[k];
     sync();
   }
 
