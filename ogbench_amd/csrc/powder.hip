@@ -664,10 +664,12 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     const int32_t* __restrict__ draws, const float* __restrict__ rand, int32_t k_steps, uint8_t* __restrict__ obs,
     float* __restrict__ reward, uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated,
     uint8_t* __restrict__ success, int32_t auto_reset, uint32_t k0, uint32_t k1, uint32_t a0, uint32_t a1,
-    uint32_t r0, uint32_t r1, const uint8_t* __restrict__ skip, int32_t refresh, int32_t chunk) {
+    uint32_t r0, uint32_t r1, const uint8_t* __restrict__ skip, int32_t refresh, int32_t chunk,
+    const int32_t* __restrict__ order, uint32_t* __restrict__ cost) {
   constexpr int C = WS * WS, CPT = FW<WS>::CPT;
   __shared__ PwFullShared<WS> sh;
   FW<WS> fw(sh);
+  const uint64_t t_start = kSparse ? 0ull : __builtin_amdgcn_s_memtime();
   // kSparse = false: one env per workgroup (e = blockIdx.x).  kSparse: the
   // envs [e0, e0 + chunk) of this workgroup that pwf_light_step_kernel did not
   // step (skip), in turn -- for launches where the light kernel is expected to
@@ -675,7 +677,10 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   // workgroup checked by one ballot instead of 4,096 exit-only workgroups of
   // 78 KB LDS, two per CU.  A separate kernel: the env loop around the forward
   // made the one-env kernel 8 % slower (A/B).
-  const int64_t e0 = kSparse ? (int64_t)blockIdx.x * chunk : (int64_t)blockIdx.x;
+  // order (one-env form, in-phase full steps): workgroups in order of the
+  // envs' last measured cost, costliest first (pwf_order_kernel), so the
+  // launch's last workgroups are short ones; results do not depend on it
+  const int64_t e0 = kSparse ? (int64_t)blockIdx.x * chunk : (order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x);
   uint64_t todo;
   if constexpr (!kSparse) {
     todo = (skip != nullptr && skip[e0]) ? 0ull : 1ull;
@@ -782,9 +787,48 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     S.elapsed[e] = el;
     S.episode[e] = ep;
   }
+  if (!kSparse && cost != nullptr && threadIdx.x == 0) cost[e] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start);
   if (!kSparse || todo == 0) break;
   __syncthreads();  // the next env's load overwrites the LDS state
   }
+}
+
+// Longest-first order of an in-phase full step's workgroups (one workgroup):
+// a counting sort of the envs by a cost key, costliest bucket first -- the
+// last measured shader cycles of the env's workgroup, or (by_task: the
+// synchronized goal-replay step) the length of its task's goal sequence.
+// The order within a bucket is whatever the LDS atomics give: only the
+// schedule depends on it.
+__global__ void __launch_bounds__(1024) pwf_order_kernel(const PowderParams* __restrict__ Pp,
+                                                         const int32_t* __restrict__ ctrl,
+                                                         const uint32_t* __restrict__ cost, int32_t n,
+                                                         int32_t by_task, int32_t* __restrict__ order) {
+  __shared__ uint32_t hist[32];
+  const int t = threadIdx.x;
+  auto key = [&](int e) -> uint32_t {
+    uint32_t c;
+    if (by_task) {
+      const int task = (ctrl[e] >> 16) & 255;
+      c = (uint32_t)Pp->seq_len[(task >= 1 && task <= Pp->num_tasks ? task : 1) - 1] >> 3;
+    } else {
+      c = cost[e] >> 13;
+    }
+    return 31u - (c < 31u ? c : 31u);  // bucket 0: costliest
+  };
+  if (t < 32) hist[t] = 0;
+  __syncthreads();
+  for (int e = t; e < n; e += 1024) atomicAdd(&hist[key(e)], 1u);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int b = 0; b < 32; ++b) {
+      const uint32_t c = hist[b];
+      hist[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < n; e += 1024) order[atomicAdd(&hist[key(e)], 1u)] = e;
 }
 
 // Render-only steps of medium/hard worlds (one step per launch).  An env at
@@ -1140,6 +1184,8 @@ struct ogbx_powder_env {
   ogbx::PowderState S{};
   uint8_t* goals = nullptr;  // easy: [num_tasks, H*W] goal ids
   uint8_t* handled = nullptr;  // medium/hard: [N] env stepped by pwf_light_step_kernel this launch
+  uint32_t* cost = nullptr;    // medium/hard: [N] shader cycles of the env's last one-env full-kernel workgroup
+  int32_t* order = nullptr;    // medium/hard: [N] workgroup -> env of an in-phase full step, costliest first
   bool light = true;           // split render-only steps into pwf_light_step_kernel
   // the render cache (S.crg / S.cb) may disagree with the state: set at create
   // and whenever a world or velocity pointer is handed out (the caller may
@@ -1286,6 +1332,9 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
     if (h == hipSuccess) h = hipMalloc(&e->S.crg, n * HW * sizeof(uint16_t));
     if (h == hipSuccess) h = hipMalloc(&e->S.cb, n * HW);
     if (h == hipSuccess) h = hipMalloc(&e->handled, n);
+    if (h == hipSuccess) h = hipMalloc(&e->cost, n * sizeof(uint32_t));
+    if (h == hipSuccess) h = hipMalloc(&e->order, n * sizeof(int32_t));
+    if (h == hipSuccess) h = hipMemset(e->cost, 0, n * sizeof(uint32_t));
     if (const char* v = std::getenv("OGBX_PWF_LIGHT")) e->light = std::atoi(v) != 0;  // A/B knob
     if (h == hipSuccess) h = hipMemset(e->S.mom, 0, n * HW);
     if (h == hipSuccess) h = hipMemset(e->S.vel, 0, n * HW * sizeof(float2));
@@ -1321,6 +1370,8 @@ ogbx_status ogbx_powder_destroy(ogbx_powder_t e) {
   (void)hipFree(e->S.cb);
   (void)hipFree(e->goals);
   (void)hipFree(e->handled);
+  (void)hipFree(e->cost);
+  (void)hipFree(e->order);
   delete e;
   return OGBX_OK;
 }
@@ -1404,11 +1455,23 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
       const int32_t chunk = kPwfSparseChunk;
       PWF_LAUNCH(pwf_step_kernel_sparse, e, (uint32_t)((e->n + chunk - 1) / chunk), stream, e->Pd, e->S, e->n,
                  action, draws, rand, k_steps, obs, reward, terminated, truncated, success, auto_reset, k0, k1, a0,
-                 a1, r0, r1, e->handled, (int32_t)e->cache_stale, chunk);
+                 a1, r0, r1, e->handled, (int32_t)e->cache_stale, chunk, (const int32_t*)nullptr, (uint32_t*)nullptr);
     } else {
+      // in-phase full step: workgroups longest first (the synchronized goal
+      // replays by task length, forward steps by last measured cost)
+      const int32_t* order = nullptr;
+      if (all_full && e->n <= INT32_MAX) {
+        const int64_t T = e->P.max_steps > 0 ? e->P.max_steps : 0;
+        const int64_t j = (auto_reset && T > 0) ? e->phase % T : e->phase;
+        const int32_t by_task = (auto_reset && T > 0 && j + 1 >= T) ? 1 : 0;
+        hipLaunchKernelGGL(pwf_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->Pd, e->S.ctrl, e->cost,
+                           (int32_t)e->n, by_task, e->order);
+        OGBX_LAUNCHED("pwf_order_kernel");
+        order = e->order;
+      }
       PWF_LAUNCH(pwf_step_kernel_dense, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps,
                  obs, reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1, r0, r1,
-                 light ? e->handled : (const uint8_t*)nullptr, (int32_t)e->cache_stale, 1);
+                 light ? e->handled : (const uint8_t*)nullptr, (int32_t)e->cache_stale, 1, order, e->cost);
     }
     OGBX_LAUNCHED("pwf_step_kernel");
     e->cache_stale = false;  // every env's cache was written by one of the two kernels
