@@ -16,6 +16,13 @@ G-rank job is the single-GPU job bit for bit (tests/test_shard_gpu.py).  No
 data-path collective; ``value`` = N x steps / time -> "scaling": "strong".
 The weak-scaling rate (65,536 envs per GPU) is reported in ``extra``.
 
+Launch: under torchrun (WORLD_SIZE set) each process is one rank; a plain
+``python bench.py --gpus N`` (N > 1, no WORLD_SIZE) starts the N rank
+processes itself before any HIP call and exits with the worst rank status.
+A WORLD_SIZE that differs from --gpus, or more nccl (RCCL) ranks than visible
+GPUs, is refused (exit 2).  ``ranks_seen`` counts the ranks an untimed
+all-gather reached.
+
 Extra fields (not ``value``): the same workload replayed from a hipGraph and
 as K fused steps per launch; ``roofline`` of maze_step_kernel (algorithmic
 87 B per env-step) from the smaller of two HIP event spans on the
@@ -27,6 +34,7 @@ count; the per-launch event-pair median beside them); ``cpu_baseline`` = the ora
 import argparse
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -34,6 +42,64 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+class LaunchError(SystemExit):
+    """A rank layout bench.py refuses to run (exit status 2, message on stderr)."""
+
+    def __init__(self, msg):
+        print(f'bench.py: {msg}', file=sys.stderr, flush=True)
+        super().__init__(2)
+
+
+def _check_world(gpus, backend, env=None):
+    """Validate the requested rank layout before anything touches the GPU.
+
+    Returns 'self-launch' when `--gpus N > 1` runs without a launcher (no
+    WORLD_SIZE in the environment), 'rank' otherwise.  Raises LaunchError when
+    the launcher's WORLD_SIZE differs from --gpus, or when the nccl (RCCL)
+    backend is asked for more ranks than there are visible GPUs (one rank per
+    GPU; the gloo backend rehearses N ranks on fewer GPUs).  Counting devices
+    does not initialise HIP on this image, so this is safe in the parent."""
+    env = os.environ if env is None else env
+    if gpus < 1:
+        raise LaunchError(f'--gpus must be >= 1, got {gpus}')
+    ws = env.get('WORLD_SIZE')
+    if ws is not None and int(ws) != gpus:
+        raise LaunchError(f'--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks; '
+                          f'run with --gpus {ws} or launch {gpus} ranks')
+    if backend == 'nccl':
+        ndev = torch.cuda.device_count()
+        if gpus > ndev:
+            raise LaunchError(f'--gpus {gpus} with the nccl (RCCL) backend needs {gpus} visible GPUs, found {ndev} '
+                              "(use --dist-backend gloo to rehearse several ranks on fewer GPUs)")
+    return 'self-launch' if ws is None and gpus > 1 else 'rank'
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(gpus, argv):
+    """`bench.py --gpus N` with no launcher: start N rank processes of this
+    same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on
+    127.0.0.1), wait for all of them and return the worst exit status.  The
+    parent never touches the GPU; rank 0 prints the one JSON line."""
+    import subprocess
+
+    port = str(_free_port())
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus), LOCAL_WORLD_SIZE=str(gpus),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    # a rank killed by signal s reports -s; the shell's 128 + s convention
+    return max((128 - rc if rc < 0 else rc) for rc in rcs), rcs
 
 
 def _dist_init(backend='nccl'):
@@ -72,6 +138,20 @@ def _max_over_ranks(x, world, dev):
     t = torch.tensor([x], dtype=torch.float64, device=dev if on_dev else 'cpu')
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def _ranks_seen(world, dev):
+    """Untimed: the number of distinct ranks an all-gather over the process
+    group reaches (1 without one): the line's proof that its n_gpus ranks ran."""
+    if world == 1:
+        return 1
+    import torch.distributed as dist
+
+    on_dev = dist.get_backend() == 'nccl'
+    mine = torch.tensor([dist.get_rank()], dtype=torch.int64, device=dev if on_dev else 'cpu')
+    got = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine)
+    return len({int(t.item()) for t in got})
 
 
 def _timed(fn, steps, world, dev, span=None):
@@ -351,7 +431,8 @@ def _cabi_allgather_check(counters, per_rank, world, dev):
 def _finish_pointmaze(args, world, rank, total, n, value, ms_per_step, kern_ms, alg_bytes, achieved, extra, env,
                       kern_info):
     result = dict(
-        metric='env steps/sec at N=65536 parallel envs, pointmaze-large, 1/2/4/8 MI355X',
+        # BASELINE.json's metric at the default N = 65,536; a --num-envs run names its own N
+        metric=f'env steps/sec at N={total} parallel envs, pointmaze-large, 1/2/4/8 MI355X',
         value=value,
         unit='env_steps/s',
         n_gpus=world,
@@ -995,18 +1076,19 @@ def main():
     ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
                     help="'gloo' rehearses the multi-rank path with ranks sharing GPUs")
     args = ap.parse_args()
+    # before any HIP call: refuse a mismatched layout, or start the N ranks
+    if _check_world(args.gpus, args.dist_backend) == 'self-launch':
+        rc, _ = _self_launch(args.gpus, sys.argv[1:])
+        sys.exit(rc)
     world, rank, local = _dist_init(args.dist_backend)
-    if world != args.gpus and rank == 0:
-        print(f'# note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE', flush=True)
     dev = torch.device('cuda', local)
-    import sys
-
     sys.path.insert(0, ROOT)
     fn = dict(pointmaze=bench_pointmaze, powder=bench_powder, **{'pointmaze-medium-n1': bench_pointmaze_n1},
               gcsample=bench_gcsample, hgcsample=bench_hgcsample, antmaze=bench_antmaze,
               **{'powder-medium': lambda *a: bench_powder(*a, level='medium'),
                  'powder-hard': lambda *a: bench_powder(*a, level='hard')})[args.workload]
     result = fn(args, world, rank, dev)
+    result['ranks_seen'] = _ranks_seen(world, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -108,9 +108,12 @@ ogbx_status ogbx_maze_destroy(ogbx_maze_t env);
 /* Number of envs of the handle. */
 int64_t ogbx_maze_num_envs(ogbx_maze_t env);
 /* Launch shape of the step/physics kernels: envs carried per 64-lane wave
- * (8, 16, 32 or 64; default 64).  Performance knob only: the contact solver
- * path is chosen per wave, so results agree to solver rounding (~1e-15), not
- * bit for bit, across values (DESIGN.md "Contact path on SIMT"). */
+ * (8, 16, 32 or 64; default 64), optionally | OGBX_EPW_REPLICATE: the wave's
+ * other lanes then step copies of its epw envs (only the first copy stores)
+ * instead of idling.  Performance knob only: every choice of the contact path
+ * is made per lane, so results are bit-identical across layouts (DESIGN.md
+ * section 4.1; tests/test_locomaze_gpu.py). */
+#define OGBX_EPW_REPLICATE 0x100
 ogbx_status ogbx_maze_set_envs_per_wave(ogbx_maze_t env, int32_t epw);
 
 /* Static description: H, W of the map, number of tasks, goal_tol

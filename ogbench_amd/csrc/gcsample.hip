@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <mutex>
 
 #include "common.h"
 
@@ -668,14 +669,16 @@ struct HgcPick {
 // entries t and t + 64 of the value / low tables (loaded when the chain
 // starts, so they arrive while it runs), and the chain's lookups are lane
 // reads instead of global loads that wait for the subgoal step counts.  Valid when both tables have at most 128 entries (subgoal
-// steps <= 127); the mask tables are 1 - (s < K), computed in line.
+// steps <= 127).  The mask tables are held the same way (the caller's tables,
+// not 1 - (s < K) recomputed, so a C-ABI host's own tables give the same
+// result as the direct ogbx_hgc_sample).
 struct HgcTables {
-  double hv0, hv1, lv0, lv1;
+  double hv0, hv1, lv0, lv1, hm0, hm1, lm0, lm1;
   bool regs;
 };
 
 __device__ __forceinline__ HgcTables hgc_tables_load(const ogbx_hgc_config& hc) {
-  HgcTables tb{0.0, 0.0, 0.0, 0.0, hc.value_subgoal_steps < 128 && hc.low_subgoal_steps < 128};
+  HgcTables tb{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, hc.value_subgoal_steps < 128 && hc.low_subgoal_steps < 128};
   const int t = (int)(threadIdx.x & 63);
   // clamped indices, every lane, no branch (a region around the loads made
   // the compiler wait for them at its end); entries past K are never looked
@@ -685,6 +688,10 @@ __device__ __forceinline__ HgcTables hgc_tables_load(const ogbx_hgc_config& hc) 
   tb.hv1 = hc.hv_reward_table[min((int64_t)t + 64, kv)];
   tb.lv0 = hc.lv_reward_table[min((int64_t)t, kl)];
   tb.lv1 = hc.lv_reward_table[min((int64_t)t + 64, kl)];
+  tb.hm0 = hc.hv_mask_table[min((int64_t)t, kv)];
+  tb.hm1 = hc.hv_mask_table[min((int64_t)t + 64, kv)];
+  tb.lm0 = hc.lv_mask_table[min((int64_t)t, kl)];
+  tb.lm1 = hc.lv_mask_table[min((int64_t)t + 64, kl)];
   return tb;
 }
 
@@ -761,8 +768,7 @@ __device__ inline HgcPick hgc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_con
   p.w[0] = hvg - idx;
   p.w[1] = hv_steps;
   if (tb.regs) {
-    // the tables' masks are 1 - (s < K) (datasets.py:535, 552)
-    p.w[2] = __double_as_longlong(hv_steps < hc.value_subgoal_steps ? 0.0 : 1.0);
+    p.w[2] = __double_as_longlong(table_lane(tb.hm0, tb.hm1, hv_steps));
     p.w[3] = __double_as_longlong(table_lane(tb.hv0, tb.hv1, hv_steps));
   } else {
     p.w[2] = __double_as_longlong(hc.hv_mask_table[hv_steps]);
@@ -774,7 +780,7 @@ __device__ inline HgcPick hgc_chain(const ogbx_gc_buffer& buf, const ogbx_gc_con
     p.w[5] = __double_as_longlong(1.0 - ls);
     p.w[6] = __double_as_longlong(ls - neg);
   } else if (tb.regs) {
-    p.w[5] = __double_as_longlong(lv_steps < hc.low_subgoal_steps ? 0.0 : 1.0);
+    p.w[5] = __double_as_longlong(table_lane(tb.lm0, tb.lm1, lv_steps));
     p.w[6] = __double_as_longlong(table_lane(tb.lv0, tb.lv1, lv_steps));
   } else {
     p.w[5] = __double_as_longlong(hc.lv_mask_table[lv_steps]);
@@ -1185,6 +1191,9 @@ struct ogbx_gc_plan_s {
   int64_t key_total = 0;
   uint64_t key_call = 0;
   int64_t hits = 0;
+  // guards pairs / npairs / key_* / hits: ctypes releases the GIL, so two
+  // host threads may call ogbx_gc_plan_sample on one plan (uncontended: ~20 ns)
+  std::mutex mu;
 };
 
 extern "C" {
@@ -1211,7 +1220,13 @@ ogbx_status ogbx_gc_plan_create(const ogbx_gc_buffer* buf, const ogbx_gc_config*
   p->hgc = hcfg != nullptr;
   if (hcfg) p->hcfg = *hcfg;
   p->lookahead = lookahead != 0;
-  if (hipGetDevice(&p->device) != hipSuccess) p->device = 0;
+  // the plan's device is the buffer's, not whichever device is current: the
+  // look-ahead selector pairs are allocated there on a stream's first call
+  hipPointerAttribute_t attr{};
+  if (hipPointerGetAttributes(&attr, buf->traj_end) == hipSuccess && attr.type == hipMemoryTypeDevice)
+    p->device = attr.device;
+  else if (hipGetDevice(&p->device) != hipSuccess)
+    p->device = 0;
   seed_key(seed, p->hgc ? kTagHgcSample : kTagGcSample, &p->k0, &p->k1);
   p->v_log_q = std::log(1.0 - (1.0 - cfg->value_discount));
   p->a_log_q = std::log(1.0 - (1.0 - cfg->actor_discount));
@@ -1257,12 +1272,15 @@ ogbx_status ogbx_gc_plan_set_batch(ogbx_gc_plan_t p, int32_t slot, const ogbx_gc
   if (hgc_out) b.hout = *hgc_out;
   b.flat4 = flat4_columns(b.cc, num_cols);
   b.set = true;
+  std::lock_guard<std::mutex> guard(p->mu);
   p->slots[slot] = b;
   return OGBX_OK;
 }
 
 ogbx_status ogbx_gc_plan_sample(ogbx_gc_plan_t p, int32_t slot, uint64_t call_index, void* stream) {
-  OGBX_CHECK(p && slot >= 0 && slot < OGBX_GC_PLAN_SLOTS && p->slots[slot].set, OGBX_EINVAL,
+  OGBX_CHECK(p, OGBX_EINVAL, "null plan");
+  std::lock_guard<std::mutex> guard(p->mu);
+  OGBX_CHECK(slot >= 0 && slot < OGBX_GC_PLAN_SLOTS && p->slots[slot].set, OGBX_EINVAL,
              "ogbx_gc_plan_sample: no batch in this slot");
   const PlanBatch& b = p->slots[slot];
   const int64_t total = b.batch * b.nb;
@@ -1344,7 +1362,11 @@ ogbx_status ogbx_gc_plan_sample(ogbx_gc_plan_t p, int32_t slot, uint64_t call_in
   return OGBX_OK;
 }
 
-int64_t ogbx_gc_plan_hits(ogbx_gc_plan_t p) { return p ? p->hits : -1; }
+int64_t ogbx_gc_plan_hits(ogbx_gc_plan_t p) {
+  if (!p) return -1;
+  std::lock_guard<std::mutex> guard(p->mu);
+  return p->hits;
+}
 
 ogbx_status ogbx_gc_plan_destroy(ogbx_gc_plan_t p) {
   if (!p) return OGBX_OK;

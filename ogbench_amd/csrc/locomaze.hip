@@ -163,15 +163,24 @@ __device__ inline void reset_one(const MazeParams& P, int32_t task, const double
 // ------------------------------------------------------------------ kernels
 
 // Env index of this lane when each 64-lane wave carries only `epw` envs
-// (epw in {16, 32, 64}).  The contact path is a long fp64 dependency chain,
+// (epw in {8, 16, 32, 64}).  The contact path is a long fp64 dependency chain,
 // so one full wave per SIMD leaves the SIMD idle; fewer envs per wave (more
 // waves per SIMD) lets the SIMD interleave independent chains.  Returns -1 for
-// idle lanes.
-__device__ inline int64_t env_of_lane(int epw) {
+// idle lanes.  With kEpwReplicate the other lanes of the wave are not idle but
+// copies: lane l steps env (l mod epw) of the wave's epw envs bit for bit (every
+// choice of the contact path is per lane), and only lanes l < epw (*writer)
+// store.  A wave then runs the union of the paths of only epw envs with all 64
+// lanes active (gfx950 issues a dependent chain ~2x slower with few active
+// lanes).
+constexpr int kEpwReplicate = 0x100;
+
+__device__ inline int64_t env_of_lane(int epw, bool* writer) {
   const int lane = threadIdx.x & 63;
-  if (lane >= epw) return -1;
+  const int e = epw & 0xFF;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  return wave * epw + lane;
+  *writer = lane < e;
+  if (lane >= e && !(epw & kEpwReplicate)) return -1;
+  return wave * e + (lane & (e - 1));
 }
 
 __global__ void __launch_bounds__(256) maze_reset_kernel(const MazeParams* __restrict__ Pp, MazeState S, int64_t n,
@@ -246,7 +255,8 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
 #ifdef OGBX_WAVE_STAMPS
   const unsigned long long ws_t0 = wall_clock64(), ws_c0 = clock64();
 #endif
-  const int64_t i = env_of_lane(epw);
+  bool writer;
+  const int64_t i = env_of_lane(epw, &writer);
   const bool live = i >= 0 && i < n;
   // one HBM round trip before the first barrier: the wall-mask entry, the
   // env's state and its first action
@@ -325,7 +335,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     const bool term = succ && P.terminate_at_goal;
     el += 1;
     const bool trunc = el >= P.max_steps;
-    const bool write = !kUntilDone || !done;
+    const bool write = writer && (!kUntilDone || !done);
     if (write) {
       __builtin_nontemporal_store(rew, &reward[o]);
       __builtin_nontemporal_store((uint8_t)term, &terminated[o]);
@@ -339,7 +349,7 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
         task = S.task[i];
         have_te = true;
       }
-      if (final_obs != nullptr) reinterpret_cast<double2*>(final_obs)[o] = make_double2(ox, oy);
+      if (final_obs != nullptr && writer) reinterpret_cast<double2*>(final_obs)[o] = make_double2(ox, oy);
       ep += 1u;
       reset_any = true;
       double r[4];
@@ -362,8 +372,9 @@ __global__ void __launch_bounds__(256) maze_step_kernel(
     x = dx_;
     y = dy_;
     el = del_;
-    steps_taken[i] = taken;
+    if (writer) steps_taken[i] = taken;
   }
+  if (!writer) return;  // a copy lane (kEpwReplicate)
   // non-temporal stores for the state and the outputs (nothing in the launch
   // reads them back): 11.37 -> 11.29 us per launch at N = 65,536 (A/B,
   // four rounds), no change at 8,192
@@ -394,7 +405,8 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
                                                             uint8_t* contact_out, int epw) {
   OGBX_POINT_MODEL(pm, (*Pp));
   __shared__ uint16_t nb_s[kMaxCells];
-  const int64_t i = env_of_lane(epw);
+  bool writer;
+  const int64_t i = env_of_lane(epw, &writer);
   const bool live = i >= 0 && i < n;
   const uint16_t nbv = nbmask_fetch(Pp);
   double x = 0.0, y = 0.0, ax = 0.0, ay = 0.0;
@@ -417,6 +429,7 @@ __global__ void __launch_bounds__(256) point_physics_kernel(const MazeParams* __
   x = x + ax;
   y = y + ay;
   int c = point_step_as(pm, nb_s, P.H, P.W, &x, &y);
+  if (!writer) return;  // a copy lane (kEpwReplicate)
   qpos_out[2 * i] = x;
   qpos_out[2 * i + 1] = y;
   if (contact_out) contact_out[i] = (uint8_t)c;
@@ -802,8 +815,9 @@ int64_t ogbx_maze_num_envs(ogbx_maze_t e) { return e ? e->n : 0; }
 
 ogbx_status ogbx_maze_set_envs_per_wave(ogbx_maze_t e, int32_t epw) {
   OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
-  OGBX_CHECK(epw == 8 || epw == 16 || epw == 32 || epw == 64, OGBX_EINVAL,
-             "envs per wave must be 8, 16, 32 or 64");
+  const int per = epw & ~kEpwReplicate;
+  OGBX_CHECK((epw & ~(kEpwReplicate | 0xFF)) == 0 && (per == 8 || per == 16 || per == 32 || per == 64), OGBX_EINVAL,
+             "envs per wave must be 8, 16, 32 or 64 (optionally | OGBX_EPW_REPLICATE)");
   e->epw = epw;
   return OGBX_OK;
 }
@@ -907,7 +921,7 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
   uint32_t k0, k1;
   seed_key(e->seed, kTagMazeReset, &k0, &k1);
   const int epw = e->epw;
-  dim3 grid(grid_for(e->n * (64 / epw), kStepBlock)), block(kStepBlock);
+  dim3 grid(grid_for(e->n * (64 / (epw & 0xFF)), kStepBlock)), block(kStepBlock);
   if (action_is_f64)
     hipLaunchKernelGGL((maze_step_kernel<true, false>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success,
@@ -983,7 +997,7 @@ ogbx_status ogbx_maze_rollout_until_done(ogbx_maze_t e, const void* action, int3
   uint32_t k0, k1;
   seed_key(e->seed, kTagMazeReset, &k0, &k1);
   const int epw = e->epw;
-  dim3 grid(grid_for(e->n * (64 / epw), kStepBlock)), block(kStepBlock);
+  dim3 grid(grid_for(e->n * (64 / (epw & 0xFF)), kStepBlock)), block(kStepBlock);
   if (action_is_f64)
     hipLaunchKernelGGL((maze_step_kernel<true, true>), grid, block, e->lds_pad, (hipStream_t)stream, e->Pd, e->S,
                        e->n, action, k_steps, obs, reward, terminated, truncated, success, nullptr, 0, k0, k1,
@@ -1022,7 +1036,7 @@ ogbx_status ogbx_point_physics(ogbx_maze_t e, const double* qpos_in, const void*
   if (n <= 0) return OGBX_OK;
   OGBX_HIP(hipSetDevice(e->device));
   const int epw = e->epw;
-  dim3 grid(grid_for(n * (64 / epw), kStepBlock)), block(kStepBlock);
+  dim3 grid(grid_for(n * (64 / (epw & 0xFF)), kStepBlock)), block(kStepBlock);
   if (action_is_f64)
     hipLaunchKernelGGL(point_physics_kernel<true>, grid, block, e->lds_pad, (hipStream_t)stream, e->Pd,
                        qpos_in, action, n, qpos_out, contact_out, epw);

@@ -481,8 +481,10 @@ class GCDataset:
             self._drop_plan()
             L = self._L
             h = ctypes.c_void_p()
-            _lib.check(L.ogbx_gc_plan_create(self._buf, self._cfg, self._hcfg_ptr(), seed, int(self._lookahead),
-                                             ctypes.byref(h)), 'gc_plan_create')
+            # the plan also takes its device from the buffer (hipPointerGetAttributes)
+            with _torch().cuda.device(self.device):
+                _lib.check(L.ogbx_gc_plan_create(self._buf, self._cfg, self._hcfg_ptr(), seed, int(self._lookahead),
+                                                 ctypes.byref(h)), 'gc_plan_create')
             self._plan, self._plan_seed = h.value, seed
             self._plan_final = weakref.finalize(self, L.ogbx_gc_plan_destroy, h.value)
             self._out_cache.clear()  # their slots belong to the old plan

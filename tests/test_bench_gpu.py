@@ -47,6 +47,24 @@ def test_default_bench_line():
     assert cb['value'] > 0 and cb['cores'] >= 1 and cb['kind'] in ('port', 'reference') and cb['sample']
 
 
+def test_two_rank_line_without_a_launcher():
+    # `bench.py --gpus 2` with no torchrun: bench.py starts both ranks itself
+    # (gloo, both on this box's GPU) and rank 0's line covers the 2-rank job
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--dist-backend', 'gloo',
+                          '--steps', '20', '--warmup', '5'], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=400)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r['n_gpus'] == 2 and r['ranks_seen'] == 2
+    assert r['extra']['eval_allgather']['ranks'] == 2
+    assert r['config']['num_envs_per_gpu'] == 32768 and r['config']['total_envs'] == 65536
+    assert r['metric'] == 'env steps/sec at N=65536 parallel envs, pointmaze-large, 1/2/4/8 MI355X'
+    assert 'cpu_baseline' not in r  # rank 0 at N = 1 only
+
+
 def test_antmaze_bench_line():
     r = _run('--workload', 'antmaze', '--steps', '1000', '--warmup', '50', '--no-cpu-baseline')
     _contract(r)

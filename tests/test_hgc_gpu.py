@@ -80,3 +80,56 @@ def test_hgc_lookahead_matches_direct_sampling(gpu, gold, cname):  # noqa: F811
             assert torch.equal(x[k], y[k]), (i, k)
         if mode != 'record':
             prev_a, prev_b = x, y
+
+
+def test_hgc_lookahead_reads_the_callers_tables(gpu, gold):  # noqa: F811
+    """The look-ahead chain looks masks and rewards up in the config's tables
+    (held in registers for K < 128), so tables other than the canonical
+    1 - (s < K) give the same batches as direct sampling."""
+    data, _, _, keys = hgc_case(gold, 'hiql', True)
+    a = HGCDataset(Dataset(data, device=gpu), dict(HGC_CONFIGS['hiql']), seed=4)
+    b = HGCDataset(Dataset(data, device=gpu), dict(HGC_CONFIGS['hiql'], lookahead=False), seed=4)
+    for h in (a, b):  # in place: the config keeps the table pointers
+        for masks, rewards in (h._hv_tab, h._lv_tab):
+            masks.copy_(torch.linspace(0.25, 0.75, masks.numel(), dtype=torch.float64, device=gpu))
+            rewards.mul_(3.0).add_(0.5)
+    assert a._lookahead and not b._lookahead
+    for i in range(4):
+        x, y = a.sample(512), b.sample(512)
+        for k in keys:
+            assert torch.equal(x[k], y[k]), (i, k)
+    assert a.ahead_hits >= 2
+
+
+def test_hgc_lookahead_long_subgoals_read_tables_in_memory(gpu, gold):  # noqa: F811
+    """subgoal_steps >= 128: the chain's table lookups fall back to memory
+    reads; still bit-identical to direct sampling and to the oracle."""
+    data, _, _, keys = hgc_case(gold, 'hiql', True)
+    cfg = dict(HGC_CONFIGS['hiql'], subgoal_steps=150)
+    a = HGCDataset(Dataset(data, device=gpu), cfg, seed=6)
+    b = HGCDataset(Dataset(data, device=gpu), dict(cfg, lookahead=False), seed=6)
+    assert a.value_subgoal_steps >= 128
+    for i in range(3):
+        x, y = a.sample(700), b.sample(700)
+        for k in keys:
+            assert torch.equal(x[k], y[k]), (i, k)
+    assert a.ahead_hits >= 1
+    out = b.sample(400, record_draws=True)
+    draws = {k: v.cpu().numpy() for k, v in out['_draws'].items()}
+    ref, _ = orc.hgc_sample(data, cfg, draws)
+    for k in keys:
+        assert np.array_equal(out[k].cpu().numpy(), ref[k]), k
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason='needs two GPUs')
+def test_sampler_on_a_non_current_device(gold):  # noqa: F811
+    """A dataset on cuda:1 with cuda:0 current: the plan allocates its
+    look-ahead buffers on the dataset's device and samples match cuda:0's."""
+    data, _, _, keys = hgc_case(gold, 'hiql', True)
+    torch.cuda.set_device(0)
+    a = HGCDataset(Dataset(data, device='cuda:1'), dict(HGC_CONFIGS['hiql']), seed=2)
+    b = HGCDataset(Dataset(data, device='cuda:0'), dict(HGC_CONFIGS['hiql']), seed=2)
+    for i in range(3):
+        x, y = a.sample(256), b.sample(256)
+        for k in keys:
+            assert torch.equal(x[k].cpu(), y[k].cpu()), (i, k)
