@@ -284,9 +284,10 @@ def bench_pointmaze(args, world, rank, dev):
     base, n = shard(total, world, rank)
     ring = args.ring
     env, actions = _maze_job(total, base, n, ring, dev)
+    views = list(actions.unbind(0))  # the ring's [n, 2] rows, indexed without a tensor op
 
     def step(i):
-        env.step(actions[i % ring])
+        env.step(views[i % ring])
 
     for i in range(args.warmup):
         step(i)

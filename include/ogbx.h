@@ -168,6 +168,15 @@ ogbx_status ogbx_maze_step(ogbx_maze_t env, const void* action, int32_t action_i
                            uint8_t* truncated, uint8_t* success, double* final_obs,
                            int32_t auto_reset, void* stream);
 
+/* The steady per-step call of a host that reuses its output buffers (the
+ * Gymnasium surface returns the same tensors every step): bind the outputs
+ * and the auto-reset flag once, then step with the action and the stream
+ * only.  ogbx_maze_step_bound(env, a, f64, s) == ogbx_maze_step(env, a, f64, 1,
+ * <bound outputs>, s); a new bind replaces the old one. */
+ogbx_status ogbx_maze_bind_step(ogbx_maze_t env, double* obs, float* reward, uint8_t* terminated,
+                                uint8_t* truncated, uint8_t* success, double* final_obs, int32_t auto_reset);
+ogbx_status ogbx_maze_step_bound(ogbx_maze_t env, const void* action, int32_t action_is_f64, void* stream);
+
 /* ---- antmaze wrapper (loco_type 1): the maze layer around caller-supplied
  * ant physics.  The ant's articulated dynamics (AntEnv.do_simulation ->
  * mujoco.mj_step x5, ogbench/locomaze/ant.py:69-95) are out of scope: the

@@ -79,6 +79,8 @@ _SIGNATURES = {
         [c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_int32, c_void_p],
     ),
+    'ogbx_maze_bind_step': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32]),
+    'ogbx_maze_step_bound': (c_int32, [c_void_p, c_void_p, c_int32, c_void_p]),
     'ogbx_antmaze_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p)]),
     'ogbx_antmaze_reset': (
         c_int32,

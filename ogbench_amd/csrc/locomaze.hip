@@ -70,6 +70,13 @@ struct ogbx_maze_env {
   double* body_qvel = nullptr;  // ant handles: f64[N,14]
   int epw = 64;  // envs per 64-lane wave of the step/physics kernels
   int lds_pad = 0;  // dynamic LDS bytes requested per step/physics workgroup
+  // outputs bound by ogbx_maze_bind_step for ogbx_maze_step_bound
+  bool bound = false;
+  double* b_obs = nullptr;
+  float* b_reward = nullptr;
+  uint8_t *b_term = nullptr, *b_trunc = nullptr, *b_succ = nullptr;
+  double* b_final = nullptr;
+  int32_t b_auto = 0;
 };
 
 namespace ogbx {
@@ -838,6 +845,18 @@ ogbx_status ogbx_diag_wave_stamps(unsigned long long* out) {
 }
 #endif
 
+#ifdef OGBX_STAGE_STAMPS
+// Diagnostic build only: the per-wave lean-stage cycle parts of the last
+// launch (point_contact.h g_wave_stages, 8 words per wave), then cleared.
+ogbx_status ogbx_diag_wave_stages(unsigned long long* out) {
+  OGBX_HIP(hipDeviceSynchronize());
+  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_stages), 4096 * 8 * sizeof(unsigned long long)));
+  static unsigned long long z[4096 * 8];
+  OGBX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_stages), z, sizeof(z)));
+  return OGBX_OK;
+}
+#endif
+
 #ifdef OGBX_PHYS_STATS
 // Diagnostic build only: read and clear the 32 physics path counters.
 ogbx_status ogbx_diag_phys_stats(unsigned long long* out16) {
@@ -906,17 +925,13 @@ ogbx_status ogbx_maze_reset(ogbx_maze_t e, const int32_t* task_id, const double*
   return OGBX_OK;
 }
 
-ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_f64,
-                           int32_t k_steps, double* obs, float* reward, uint8_t* terminated,
-                           uint8_t* truncated, uint8_t* success, double* final_obs,
-                           int32_t auto_reset, void* stream) {
-  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
-  OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
-  OGBX_CHECK(e->P.loco_type == 0, OGBX_EINVAL,
-             "only the point-mass dynamics are implemented (ant/humanoid are wrapper-only)");
-  OGBX_CHECK(action && obs && reward && terminated && truncated && success, OGBX_EINVAL,
-             "ogbx_maze_step: null argument");
-  OGBX_CHECK(k_steps >= 1, OGBX_EINVAL, "k_steps must be >= 1");
+}  // extern "C"
+
+namespace {
+// the launch of ogbx_maze_step / ogbx_maze_step_bound (arguments validated)
+ogbx_status maze_step_launch(ogbx_maze_t e, const void* action, int32_t action_is_f64, int32_t k_steps, double* obs,
+                             float* reward, uint8_t* terminated, uint8_t* truncated, uint8_t* success,
+                             double* final_obs, int32_t auto_reset, void* stream) {
   OGBX_HIP(hipSetDevice(e->device));
   uint32_t k0, k1;
   seed_key(e->seed, kTagMazeReset, &k0, &k1);
@@ -932,6 +947,49 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
                        final_obs, auto_reset, k0, k1, epw, nullptr);
   OGBX_LAUNCHED("maze_step_kernel");
   return OGBX_OK;
+}
+}  // namespace
+
+extern "C" {
+
+ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_f64,
+                           int32_t k_steps, double* obs, float* reward, uint8_t* terminated,
+                           uint8_t* truncated, uint8_t* success, double* final_obs,
+                           int32_t auto_reset, void* stream) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
+  OGBX_CHECK(e->P.loco_type == 0, OGBX_EINVAL,
+             "only the point-mass dynamics are implemented (ant/humanoid are wrapper-only)");
+  OGBX_CHECK(action && obs && reward && terminated && truncated && success, OGBX_EINVAL,
+             "ogbx_maze_step: null argument");
+  OGBX_CHECK(k_steps >= 1, OGBX_EINVAL, "k_steps must be >= 1");
+  return maze_step_launch(e, action, action_is_f64, k_steps, obs, reward, terminated, truncated, success, final_obs,
+                          auto_reset, stream);
+}
+
+ogbx_status ogbx_maze_bind_step(ogbx_maze_t e, double* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+                                uint8_t* success, double* final_obs, int32_t auto_reset) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->P.loco_type == 0, OGBX_EINVAL,
+             "only the point-mass dynamics are implemented (ant/humanoid are wrapper-only)");
+  OGBX_CHECK(obs && reward && terminated && truncated && success, OGBX_EINVAL, "ogbx_maze_bind_step: null output");
+  e->b_obs = obs;
+  e->b_reward = reward;
+  e->b_term = terminated;
+  e->b_trunc = truncated;
+  e->b_succ = success;
+  e->b_final = final_obs;
+  e->b_auto = auto_reset;
+  e->bound = true;
+  return OGBX_OK;
+}
+
+ogbx_status ogbx_maze_step_bound(ogbx_maze_t e, const void* action, int32_t action_is_f64, void* stream) {
+  OGBX_CHECK(e != nullptr && action != nullptr, OGBX_EINVAL, "ogbx_maze_step_bound: null argument");
+  OGBX_CHECK(e->bound, OGBX_ESTATE, "ogbx_maze_step_bound: no outputs bound (ogbx_maze_bind_step)");
+  OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
+  return maze_step_launch(e, action, action_is_f64, 1, e->b_obs, e->b_reward, e->b_term, e->b_trunc, e->b_succ,
+                          e->b_final, e->b_auto, stream);
 }
 
 ogbx_status ogbx_antmaze_state(ogbx_maze_t e, double** body_qpos, double** body_qvel) {

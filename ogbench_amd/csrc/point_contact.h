@@ -518,6 +518,29 @@ __device__ __forceinline__ double band_u(const PointModel& pm, double d) {
 __device__ unsigned long long g_wave_paths[4096];
 #endif
 
+#ifdef OGBX_STAGE_STAMPS
+// Diagnostic build only: shader-clock cycles per part of the lean stage,
+// summed over the step's 20 stages, per wave (first active lane stores):
+// 0 RK offsets + next collision, 1 piece solve, 2 edge mask (+ the first
+// stage's Newton step), 3 next slots (band gains, weights), 4 active-set
+// iterations, 5 RK update; 6 iteration trips, 7 stages that iterated.  Each
+// stamp is an s_memtime between scheduling barriers, so the parts are priced
+// in issue order (a part's stall on an earlier part's latency counts to it)
+// and the build is slower than the product; the parts' proportions are the
+// reading, not their sum.
+__device__ unsigned long long g_wave_stages[4096 * 8];
+#define OGBX_SS_AT(acc)                              \
+  do {                                               \
+    __builtin_amdgcn_sched_barrier(0);               \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);               \
+    acc += _t - ss_t;                                \
+    ss_t = _t;                                       \
+  } while (0)
+#else
+#define OGBX_SS_AT(acc) ((void)0)
+#endif
+
 // The slots of one stage, with the stage's normal equations SCALED: with
 // u'_s = (1 - imp_s) / (dmax - dmin) of slot s (band_u) and
 // P = diag (dmax - dmin) u'_0 u'_1 u'_2, the weight of slot s becomes
@@ -550,35 +573,42 @@ __device__ __forceinline__ double kp_or_far(bool on, double kp) {
 // (a_e the edge activities; PieceWeights carries A2 = a0+a1+a2 and C2 = a2).
 __device__ __forceinline__ void local_piece_min(const LocalSlots& c, const PieceWeights& p, double vx, double vy,
                                                 double* ux, double* uy) {
-#pragma clang fp contract(fast)
+  // Every fused multiply-add is written out (no contraction pragma here or in
+  // local_corner_res): the three call sites -- the stage's solve, the first
+  // stage's Newton step and the active-set iterations -- then issue the same
+  // arithmetic.  A settled lane that its wave's iterations rerun (the trip
+  // count is wave-uniform) must reproduce its values bit for bit, or its
+  // result would depend on which envs share its wave; with contraction left to
+  // the compiler the sites fused differently (1 ulp at 8 envs per wave,
+  // scripts/probe_epw_diff.py, round 6).
   const double w0 = c.w0, w1 = c.w1, w2 = c.w2;
   const double nx = c.nx2, ny = c.ny2;
   const double c2 = fma(nx, nx, -(ny * ny)), s2 = (nx + nx) * ny;
   const double A = w2 * p.A2, B = w2 * p.D2, C = w2 * p.C2;  // B = -(a1 - a0) w2
   const double X = fma(C, c2, -(B * s2));
   const double mpA = c.mp + A;
-  double h00 = fma(w0, p.S0, fma(w1, p.T1, mpA)) + X;
-  double h11 = fma(w0, p.T0, fma(w1, p.S1, mpA)) - X;
+  const double h00 = fma(w0, p.S0, fma(w1, p.T1, mpA)) + X;
+  const double h11 = fma(w0, p.T0, fma(w1, p.S1, mpA)) - X;
   double h01 = fma(w0, p.D0, -(w1 * p.D1));
   h01 = fma(C, s2, h01);
   h01 = fma(B, c2, h01);
   const double g0 = w0 * c.kp0, g1 = w1 * c.kp1;
-  double r0 = c.mbp * vx + g0 * p.S0 - g1 * p.D1;
-  double r1 = c.mbp * vy + g0 * p.D0 + g1 * p.S1;
+  double r0 = fma(-g1, p.D1, fma(g0, p.S0, c.mbp * vx));
+  double r1 = fma(g1, p.S1, fma(g0, p.D0, c.mbp * vy));
   const double WS = A + C, k2 = c.kp2;
-  r0 -= k2 * (WS * nx - B * ny);
-  r1 -= k2 * (WS * ny + B * nx);
-  const double idet = fast_recip(h00 * h11 - h01 * h01);
-  *ux = (h11 * r0 - h01 * r1) * idet;
-  *uy = (h00 * r1 - h01 * r0) * idet;
+  r0 = fma(-k2, fma(WS, nx, -(B * ny)), r0);
+  r1 = fma(-k2, fma(WS, ny, B * nx), r1);
+  const double idet = fast_recip(fma(h00, h11, -(h01 * h01)));
+  *ux = fma(h11, r0, -(h01 * r1)) * idet;
+  *uy = fma(h00, r1, -(h01 * r0)) * idet;
 }
 
 // The corner slot's residual pair (a = n.u + kp, b = t.u) at U: one
-// definition for the mask and the settled test, so both see the same values.
+// definition for the mask and the settled test, so both see the same values
+// (fused explicitly, as local_piece_min).
 __device__ __forceinline__ void local_corner_res(const LocalSlots& c, double ux, double uy, double* a, double* b) {
-#pragma clang fp contract(fast)
-  *a = c.nx2 * ux + (c.ny2 * uy + c.kp2);
-  *b = c.nx2 * uy - c.ny2 * ux;
+  *a = fma(c.nx2, ux, fma(c.ny2, uy, c.kp2));
+  *b = fma(c.nx2, uy, -(c.ny2 * ux));
 }
 
 // Active-edge mask at U (local role layout, bits as edge_mask).
@@ -651,6 +681,10 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
 #ifdef OGBX_WAVE_STAMPS
   unsigned long long g_wpath = 0;
 #endif
+#ifdef OGBX_STAGE_STAMPS
+  unsigned long long ss0 = 0, ss1 = 0, ss2 = 0, ss3 = 0, ss4 = 0, ss5 = 0, ss6 = 0, ss7 = 0;
+  unsigned long long ss_t = __builtin_amdgcn_s_memtime();
+#endif
   const double h = pm.h;
   const LeanSides L = lean_sides(pm, fr, x, y);
   uint32_t ehi = 0;
@@ -698,8 +732,10 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
     }
     LeanHit k;
     if (more) local_collide(L, nex, ney, k, ehi);
+    OGBX_SS_AT(ss0);
     double ux, uy;
     local_piece_min(c, pw, vsx, vsy, &ux, &uy);
+    OGBX_SS_AT(ss1);
     uint32_t A2 = local_edge_mask(c, ux, uy);
     if (e == 0) {
       // The first stage's warm start (every penetrating edge active) is exact
@@ -715,8 +751,10 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
     // per-edge expected sign words, v_bitop3-merged -- 5 fewer instructions
     // per stage, no vcc hazards -- measured 11.55 -> 12.2 us per launch)
     bool done = A2 == act;
+    OGBX_SS_AT(ss2);
     LocalSlots cn;
     if (more) local_slots(pm, k, cn);
+    OGBX_SS_AT(ss3);
 #ifdef OGBX_PHYS_STATS
     if (!done) {
       const int pc = __builtin_popcount(A2 ^ act);
@@ -738,6 +776,10 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
 #pragma unroll 1
       for (int it = 0; it < kLeanIters; ++it) {
         OGBX_WPATH(20);
+#ifdef OGBX_STAGE_STAMPS
+        ss6 += 1;
+        ss7 += it == 0;
+#endif
 #ifdef OGBX_PHYS_STATS
         if (!done) OGBX_STAT(4);
         trips += !done;
@@ -754,6 +796,7 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
       if (trips == 1) OGBX_STAT(5);
 #endif
     }
+    OGBX_SS_AT(ss4);
     double fx, fy;
     {
 #pragma clang fp contract(fast)
@@ -779,7 +822,18 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
       }
     }
     if (more) c = cn;
+    OGBX_SS_AT(ss5);
   }
+#ifdef OGBX_STAGE_STAMPS
+  {
+    const unsigned long long b = __ballot(1);
+    const unsigned w = (unsigned)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (w < 4096 && (int)(threadIdx.x & 63) == __ffsll((long long)b) - 1) {
+      unsigned long long* o = g_wave_stages + 8 * w;
+      o[0] = ss0, o[1] = ss1, o[2] = ss2, o[3] = ss3, o[4] = ss4, o[5] = ss5, o[6] = ss6, o[7] = ss7;
+    }
+  }
+#endif
   *bail = bl | !(ehi < kLeanEhiLimit);
   x = fma(L.sxd, pm.box_hxy - Ex, L.cx);
   y = fma(L.syd, pm.box_hxy - Ey, L.cy);

@@ -621,6 +621,9 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
   if (mask != nullptr && mask[e] == 0) return;
   FW<WS> fw(sh);
+#ifdef OGBX_PWF_RULE_STAMPS
+  fw.diag_env = e;
+#endif
   pwf_tables(sh, Pp);
   const int ne = Pp->num_elems, xy = Pp->xy_size, nt = Pp->num_tasks;
   const uint32_t ep = S.episode[e] + 1u;
@@ -697,6 +700,9 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   const int64_t e = kSparse ? e0 + __builtin_ctzll(todo) : e0;
   todo &= todo - 1ull;
   const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
+#ifdef OGBX_PWF_RULE_STAMPS
+  fw.diag_env = e;
+#endif
   fw.load(S.world + (size_t)e * C, S.mom + (size_t)e * C, S.vel + (size_t)e * C);
 #pragma unroll
   for (int k = 0; k < CPT; ++k) sh.g[fw.cell(k)] = S.goal_env[(size_t)e * C + fw.cell(k)];
@@ -978,6 +984,9 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   __shared__ PwFullShared<WS> sh;
   FW<WS> fw(sh);
   const int64_t e = blockIdx.x;
+#ifdef OGBX_PWF_RULE_STAMPS
+  fw.diag_env = e;
+#endif
   pwf_tables(sh, Pp);
   const float* w = in + (size_t)e * 9 * C;
 #pragma unroll

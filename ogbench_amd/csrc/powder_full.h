@@ -112,14 +112,18 @@ __device__ __forceinline__ bool in_set(uint32_t mask, uint32_t id) { return (mas
 
 #ifdef OGBX_PWF_RULE_STAMPS
 // Diagnostic build only: shader-clock cycles per rule, accumulated per env
-// (workgroup) over every forward: slots 0 presence + rands, 1 stone, 2 gravity,
-// 3 sand, 4 fluid, 5 ice, 6 water, 7 fire, 8 plant, 9 velocity, 15 forwards.
+// over every forward: slots 0 presence + rands, 1 stone, 2 gravity, 3 sand,
+// 4 fluid, 5 ice, 6 water, 7 fire, 8 plant, 9 velocity, 15 forwards.  Keyed
+// by the env the kernel set in FullWorld::diag_env (not blockIdx.x: with the
+// longest-first order a workgroup is a slot of that step's sort, and a sparse
+// workgroup steps several envs).
 __device__ unsigned long long g_pwf_rule[4096 * 16];
+#define OGBX_RS_ENV (diag_env >= 0 && diag_env < 4096)
 #define OGBX_RS_BEGIN() unsigned long long _rs_prev = __builtin_amdgcn_s_memtime()
 #define OGBX_RS(slot)                                                                         \
   do {                                                                                        \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                               \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_pwf_rule[blockIdx.x * 16 + (slot)] += _t - _rs_prev; \
+    if (threadIdx.x == 0 && OGBX_RS_ENV) g_pwf_rule[diag_env * 16 + (slot)] += _t - _rs_prev; \
     _rs_prev = _t;                                                                            \
   } while (0)
 // sub-stamps inside one rule (slots 10..14; the velocity rule's parts)
@@ -128,7 +132,7 @@ __device__ unsigned long long g_pwf_rule[4096 * 16];
 #define OGBX_RS_AT(prev, slot)                                                                \
   do {                                                                                        \
     const unsigned long long _t = __builtin_amdgcn_s_memtime();                               \
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_pwf_rule[blockIdx.x * 16 + (slot)] += _t - (prev); \
+    if (threadIdx.x == 0 && OGBX_RS_ENV) g_pwf_rule[diag_env * 16 + (slot)] += _t - (prev); \
     (prev) = _t;                                                                              \
   } while (0)
 #else
@@ -161,6 +165,9 @@ struct FullWorld {
   using Codes = typename std::conditional<(CPT <= 4), uint32_t, uint64_t>::type;
   PwFullShared<WS>& s;
   mutable int r0, col;
+#ifdef OGBX_PWF_RULE_STAMPS
+  int64_t diag_env = -1;  // the env the rule stamps are keyed by (set by the kernel)
+#endif
   __device__ __forceinline__ explicit FullWorld(PwFullShared<WS>& sh)
       : s(sh),
         r0(W == 64 ? __builtin_amdgcn_readfirstlane((int)threadIdx.x / W) : (int)threadIdx.x / W),
@@ -1073,7 +1080,7 @@ struct FullWorld {
     sync();
     OGBX_RS(0);
 #ifdef OGBX_PWF_RULE_STAMPS
-    if (threadIdx.x == 0 && blockIdx.x < 4096) g_pwf_rule[blockIdx.x * 16 + 15] += 1;
+    if (threadIdx.x == 0 && OGBX_RS_ENV) g_pwf_rule[diag_env * 16 + 15] += 1;
     forward_masked(P, _rs_prev);
 #else
     forward_masked(P);

@@ -220,6 +220,42 @@ class Dataset(dict):
         self._seed = None
         self._calls = 0
 
+    # column replacements bump _gen, so that a sampler's per-call staleness
+    # check is one int compare plus the packed columns' version counters
+    _gen = 0
+
+    def __setitem__(self, key, value):
+        self._gen += 1
+        super().__setitem__(key, value)
+
+    def __delitem__(self, key):
+        self._gen += 1
+        super().__delitem__(key)
+
+    def update(self, *a, **kw):
+        self._gen += 1
+        super().update(*a, **kw)
+
+    def pop(self, *a):
+        self._gen += 1
+        return super().pop(*a)
+
+    def popitem(self):
+        self._gen += 1
+        return super().popitem()
+
+    def clear(self):
+        self._gen += 1
+        super().clear()
+
+    def setdefault(self, key, default=None):
+        self._gen += 1
+        return super().setdefault(key, default)
+
+    def __ior__(self, other):
+        self._gen += 1
+        return super().__ior__(other)
+
     def copy(self, add_or_replace=None):
         d = dict(self)
         if add_or_replace:
@@ -396,9 +432,12 @@ class GCDataset:
         ds = self.dataset
         # fast check (every sample() call): the packed columns are the same
         # tensor objects with the same version counters
-        if (all(map(operator.is_, map(ds.get, self._rec_keys), self._rec_tensors))
-                and tuple(map(_VERSION, self._rec_tensors)) == self._rec_versions):
-            return
+        gen = getattr(ds, '_gen', None)
+        if (gen is not None and gen == self._rec_gen) or \
+                all(map(operator.is_, map(ds.get, self._rec_keys), self._rec_tensors)):
+            if tuple(map(_VERSION, self._rec_tensors)) == self._rec_versions:
+                self._rec_gen = gen
+                return
         stale = False
         for k, t, _, _, ver in self._rec_src:
             cur = ds.get(k)
@@ -419,6 +458,7 @@ class GCDataset:
         self._rec_keys = tuple(e[0] for e in self._rec_src)
         self._rec_tensors = tuple(e[1] for e in self._rec_src)
         self._rec_versions = tuple(e[4] for e in self._rec_src)
+        self._rec_gen = None  # set by the next clean check (Dataset._gen of a verified state)
 
     def _column(self, src_key, dst, select):
         """Descriptor of one gathered column (from the row record when the key

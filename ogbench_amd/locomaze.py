@@ -183,6 +183,15 @@ class MazeEnv:
                           _lib.ptr(self._trunc), _lib.ptr(self._succ),
                           _lib.ptr(self._final_obs))  # written only by an auto-reset
         self._ant_qshape, self._ant_vshape, self._f64 = torch.Size((n, 15)), torch.Size((n, 14)), torch.float64
+        # the steady step (step()'s fast path): outputs bound once in the
+        # handle (ogbx_maze_bind_step, re-bound when auto_reset changes), then
+        # one 4-argument call per step with the raw stream handle
+        self._bound_auto = None
+        self._step_bound = L.ogbx_maze_step_bound
+        self._raw_stream = torch._C._cuda_getCurrentRawStream
+        self._Tensor, self._f32, self._f64t = torch.Tensor, torch.float32, torch.float64
+        self._act_shape = torch.Size((n, 2))
+        self._is_point = loco_env_type == 'point'
         self._term_b = self._term.view(torch.bool)
         self._trunc_b = self._trunc.view(torch.bool)
         self._succ_b = self._succ.view(torch.bool)
@@ -482,21 +491,33 @@ class MazeEnv:
         action: [N,2] float32 (NEP-50 float32 scaling) or float64.
         Returns (obs, reward, terminated, truncated, info) with info['success'].
         """
-        if self._loco_env_type != 'point':
-            raise NotImplementedError(
-                f'{self._loco_env_type} dynamics are out of scope: advance body_state() with your physics engine '
-                'and call wrap_step(qpos, qvel)')
-        a = self._action(action)
-        if a.shape != (self.num_envs, 2):
-            raise ValueError(f'action must have shape ({self.num_envs}, 2), got {tuple(a.shape)}')
-        _lib.check(
-            self._L.ogbx_maze_step(
-                self._h, a.data_ptr(), int(a.dtype == _torch().float64), 1, *self._step_out,
-                int(self.auto_reset), self._stream()),
-            'step',
-        )
+        a = action
+        # fast path: a contiguous [N, 2] float32 / float64 tensor on this device
+        # (the common case; a few attribute reads instead of _action's checks)
+        if (type(a) is self._Tensor and self._is_point and a.is_cuda and a.shape == self._act_shape
+                and a.get_device() == self._dev_idx and a.is_contiguous()):
+            dt = a.dtype
+            f64 = 0 if dt is self._f32 else (1 if dt is self._f64t else -1)
+        else:
+            f64 = -1
+        if f64 < 0:
+            if not self._is_point:
+                raise NotImplementedError(
+                    f'{self._loco_env_type} dynamics are out of scope: advance body_state() with your physics '
+                    'engine and call wrap_step(qpos, qvel)')
+            a = self._action(action)
+            if a.shape != (self.num_envs, 2):
+                raise ValueError(f'action must have shape ({self.num_envs}, 2), got {tuple(a.shape)}')
+            f64 = int(a.dtype == self._f64t)
+        auto = self._auto_i
+        if auto != self._bound_auto:
+            _lib.check(self._L.ogbx_maze_bind_step(self._h, *self._step_out, auto), 'step')
+            self._bound_auto = auto
+        st = self._step_bound(self._h, a.data_ptr(), f64, self._raw_stream(self._dev_idx))
+        if st:
+            _lib.check(st, 'step')
         info = {'success': self._succ_b}
-        if self.auto_reset:
+        if auto:
             info['final_observation'] = self._final_obs
         return self._obs, self._reward, self._term_b, self._trunc_b, info
 

@@ -437,7 +437,7 @@ def test_results_do_not_depend_on_envs_per_wave(gpu):
     q = np.stack([c[:, 1] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n), c[:, 0] * 4.0 - 4 + rng.uniform(-1.9, 1.9, n)], 1)
     acts = torch.tensor(rng.uniform(-1, 1, (K, n, 2)).astype(np.float32)).to(gpu)
     res = {}
-    for epw in (64, 32, 16, 32 | 0x100, 16 | 0x100, 8 | 0x100):  # 0x100: OGBX_EPW_REPLICATE
+    for epw in (64, 32, 16, 8, 32 | 0x100, 16 | 0x100, 8 | 0x100):  # 0x100: OGBX_EPW_REPLICATE
         env = _env(gpu, n, max_episode_steps=9, auto_reset=True)
         _lib.check(env._L.ogbx_maze_set_envs_per_wave(env._h, epw))
         env.reset(seed=5)
