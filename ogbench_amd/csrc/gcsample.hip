@@ -30,17 +30,6 @@ struct GcColumns {
   ogbx_gc_column c[kGcMaxCols];
 };
 
-// The column table as a kernel argument: by value (1,280 bytes of kernel
-// arguments; the direct C-ABI calls) or as a pointer to a device copy that a
-// sampler plan prepared once per output batch (8 bytes: the host's launch
-// cost grows with the argument size, 2.5 -> 3.4 us per launch on ROCm 7,
-// profiles/r06_launch_host.txt, and a steady sample(1024) call is host-bound).
-struct GcColumnsRef {
-  const GcColumns* __restrict__ p;
-};
-__device__ __forceinline__ const GcColumns& cols_of(const GcColumns& c) { return c; }
-__device__ __forceinline__ const GcColumns& cols_of(const GcColumnsRef& r) { return *r.p; }
-
 __device__ inline uint64_t bounded64(uint32_t hi, uint32_t lo, uint64_t n) {
   const uint64_t u = ((uint64_t)hi << 32) | lo;
   return __umul64hi(u, n);
@@ -441,14 +430,13 @@ __device__ inline GcPick gc_wave_chain(const ogbx_gc_buffer& buf, const ogbx_gc_
 constexpr int kGcAheadWords = OGBX_GC_AHEAD_WORDS;
 constexpr int64_t kGcAheadMaxSamples = 1024;
 
-template <bool kHit, class Cols = GcColumns>
+template <bool kHit>
 __global__ void __launch_bounds__(256) gc_ahead_kernel(
-    ogbx_gc_buffer buf, ogbx_gc_config cfg, Cols cols_arg, int32_t num_cols, uint32_t k0, uint32_t k1,
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, GcColumns cols, int32_t num_cols, uint32_t k0, uint32_t k1,
     uint32_t call_lo, uint32_t call_hi, uint32_t next_lo, uint32_t next_hi, double v_log_q, double a_log_q,
     const int64_t* __restrict__ ahead_in, int64_t* __restrict__ ahead_out, int64_t* idxs_out, int64_t* vgoal_out,
     int64_t* agoal_out, double* masks, double* rewards, bool flat4) {
   __shared__ int64_t sel[4][kGcMaxTile];
-  const GcColumns& cols = cols_of(cols_arg);
   const int64_t s = xcd_tile();
   const int t = (int)threadIdx.x;
   auto publish = [&](const GcPick& p) {
@@ -826,14 +814,13 @@ constexpr int kHgcAheadWords = OGBX_HGC_AHEAD_WORDS;
 static_assert(kHgcAheadWords >= kHgcSel + 9, "HGC look-ahead record: 10 selectors + 9 scalars");
 
 // HGCDataset.sample with look-ahead (gc_ahead_kernel's scheme).
-template <bool kHit, class Cols = GcColumns>
+template <bool kHit>
 __global__ void __launch_bounds__(256) hgc_ahead_kernel(
-    ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, Cols cols_arg, int32_t num_cols, uint32_t k0,
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, GcColumns cols, int32_t num_cols, uint32_t k0,
     uint32_t k1, uint32_t call_lo, uint32_t call_hi, uint32_t next_lo, uint32_t next_hi, double v_log_q,
     double a_log_q, double l_log_q, const int64_t* __restrict__ ahead_in, int64_t* __restrict__ ahead_out,
     ogbx_hgc_outputs o, bool flat4) {
   __shared__ int64_t sel[kHgcSel][kGcMaxTile];
-  const GcColumns& cols = cols_of(cols_arg);
   const int64_t s = xcd_tile();
   const int t = (int)threadIdx.x;
   // scalar word j (0..8) of a record -> its output (static j: no pointer array)
@@ -1179,11 +1166,7 @@ struct PlanBatch {
   double *masks = nullptr, *rewards = nullptr;
   ogbx_hgc_outputs hout{};
   bool flat4 = false;
-  GcColumns* cc_dev = nullptr;  // device copy of cc (a plan ring entry), once uploaded
 };
-// Device column tables of a plan: a ring, one entry per prepared batch,
-// uploaded (stream-ordered) by the batch's first sample call.
-constexpr int kPlanRing = 256;
 
 struct PlanPair {
   void* stream = nullptr;
@@ -1208,14 +1191,6 @@ struct ogbx_gc_plan_s {
   int64_t key_total = 0;
   uint64_t key_call = 0;
   int64_t hits = 0;
-  // the device column-table ring and the one stream the plan has seen: on a
-  // single stream a ring entry is rewritten (hipMemcpyAsync on that stream)
-  // only after every earlier launch that read it, by stream order; a plan
-  // used from a second stream launches with the table by value from then on
-  GcColumns* ring = nullptr;
-  int ring_next = 0;
-  void* only_stream = nullptr;
-  bool multi_stream = false;
   // guards pairs / npairs / key_* / hits: ctypes releases the GIL, so two
   // host threads may call ogbx_gc_plan_sample on one plan (uncontended: ~20 ns)
   std::mutex mu;
@@ -1298,7 +1273,7 @@ ogbx_status ogbx_gc_plan_set_batch(ogbx_gc_plan_t p, int32_t slot, const ogbx_gc
   b.flat4 = flat4_columns(b.cc, num_cols);
   b.set = true;
   std::lock_guard<std::mutex> guard(p->mu);
-  p->slots[slot] = b;  // cc_dev = nullptr: uploaded by the first sample call
+  p->slots[slot] = b;
   return OGBX_OK;
 }
 
@@ -1307,11 +1282,9 @@ ogbx_status ogbx_gc_plan_sample(ogbx_gc_plan_t p, int32_t slot, uint64_t call_in
   std::lock_guard<std::mutex> guard(p->mu);
   OGBX_CHECK(slot >= 0 && slot < OGBX_GC_PLAN_SLOTS && p->slots[slot].set, OGBX_EINVAL,
              "ogbx_gc_plan_sample: no batch in this slot");
-  PlanBatch& b = p->slots[slot];
+  const PlanBatch& b = p->slots[slot];
   const int64_t total = b.batch * b.nb;
   hipStream_t s = (hipStream_t)stream;
-  if (p->only_stream == nullptr) p->only_stream = stream ? stream : (void*)1;
-  else if (p->only_stream != (stream ? stream : (void*)1)) p->multi_stream = true;
   const uint32_t clo = (uint32_t)call_index, chi = (uint32_t)(call_index >> 32);
   if (!p->lookahead || total > kGcAheadMaxSamples) {
     p->key_valid = false;
@@ -1368,45 +1341,15 @@ ogbx_status ogbx_gc_plan_sample(ogbx_gc_plan_t p, int32_t slot, uint64_t call_in
     out = p->pairs[pi].buf[which];
   }
   const uint64_t next = call_index + 1;
-  if (!p->multi_stream && b.cc_dev == nullptr) {
-    if (p->ring == nullptr) {
-      int cur = 0;
-      OGBX_HIP(hipGetDevice(&cur));
-      if (cur != p->device) OGBX_HIP(hipSetDevice(p->device));
-      const hipError_t e0 = hipMalloc(&p->ring, kPlanRing * sizeof(GcColumns));
-      if (cur != p->device) (void)hipSetDevice(cur);
-      if (e0 != hipSuccess) {
-        p->ring = nullptr;
-        return hip_fail(e0, "hipMalloc (plan column tables)");
-      }
-    }
-    GcColumns* entry = p->ring + (p->ring_next++ % kPlanRing);
-    OGBX_HIP(hipMemcpyAsync(entry, &b.cc, sizeof(GcColumns), hipMemcpyHostToDevice, s));
-    b.cc_dev = entry;
-  }
-  if (p->multi_stream) {  // the table by value (see ogbx_gc_plan_s::ring)
-    if (p->hgc) {
-      const auto kern = in ? hgc_ahead_kernel<true> : hgc_ahead_kernel<false>;
-      hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, p->hcfg, b.cc, b.ncols, p->k0,
-                         p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q, p->a_log_q, p->l_log_q,
-                         in, out, b.hout, b.flat4);
-      OGBX_LAUNCHED("hgc_ahead_kernel");
-    } else {
-      const auto kern = in ? gc_ahead_kernel<true> : gc_ahead_kernel<false>;
-      hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, b.cc, b.ncols, p->k0, p->k1,
-                         clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q, p->a_log_q, in, out, b.idxs,
-                         b.vg, b.ag, b.masks, b.rewards, b.flat4);
-      OGBX_LAUNCHED("gc_ahead_kernel");
-    }
-  } else if (p->hgc) {
-    const auto kern = in ? hgc_ahead_kernel<true, GcColumnsRef> : hgc_ahead_kernel<false, GcColumnsRef>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, p->hcfg, GcColumnsRef{b.cc_dev},
+  if (p->hgc) {
+    const auto kern = in ? hgc_ahead_kernel<true> : hgc_ahead_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, p->hcfg, b.cc,
                        b.ncols, p->k0, p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q,
                        p->a_log_q, p->l_log_q, in, out, b.hout, b.flat4);
     OGBX_LAUNCHED("hgc_ahead_kernel");
   } else {
-    const auto kern = in ? gc_ahead_kernel<true, GcColumnsRef> : gc_ahead_kernel<false, GcColumnsRef>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, GcColumnsRef{b.cc_dev}, b.ncols,
+    const auto kern = in ? gc_ahead_kernel<true> : gc_ahead_kernel<false>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, b.cc, b.ncols,
                        p->k0, p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q, p->a_log_q, in,
                        out, b.idxs, b.vg, b.ag, b.masks, b.rewards, b.flat4);
     OGBX_LAUNCHED("gc_ahead_kernel");
@@ -1428,7 +1371,6 @@ int64_t ogbx_gc_plan_hits(ogbx_gc_plan_t p) {
 ogbx_status ogbx_gc_plan_destroy(ogbx_gc_plan_t p) {
   if (!p) return OGBX_OK;
   hipError_t err = hipSuccess;
-  if (p->ring) err = hipFree(p->ring);  // waits for in-flight launches
   for (int i = 0; i < p->npairs; ++i)
     for (int k = 0; k < 2; ++k)
       if (p->pairs[i].buf[k]) {

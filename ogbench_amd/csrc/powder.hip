@@ -105,6 +105,30 @@ struct PowderState {
   uint8_t* cb;       // [N, H*W]
 };
 
+// Next-episode reset states prepared ahead (medium / hard, ogbx_powder_step):
+// an auto-reset's goal replay and initial state depend only on the env's
+// task, its next episode number and the seed (Philox), not on the episode
+// being played, so pwf_prepare_kernel computes them on a low-priority side
+// stream during the episode, a few replay ops per launch, into these shadow
+// buffers.  The synchronized auto-reset step then loads them instead of
+// replaying.  tag / ep / q: the host epoch the shadow belongs to (bumped by
+// every reset or seed change), the episode and task it is for, and the next
+// replay op (q > len: complete).  use != 0 only on a step the host
+// joined the side stream before; any mismatch replays in line, so results
+// never depend on the schedule.
+struct PwPrep {
+  uint8_t* world;
+  int8_t* mom;
+  float2* vel;
+  uint8_t* goal;
+  uint32_t* tag;
+  uint32_t* ep;
+  int32_t* q;
+  int32_t* task;
+  uint32_t epoch;
+  int32_t use;
+};
+
 template <int WS>
 struct Geo {
   static constexpr int H = WS, W = WS, CELLS = WS * WS, CPT = CELLS / 256, NW = CPT / 4;
@@ -653,6 +677,54 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
   }
 }
 
+// Up to `ops` replay ops of every env's next-episode reset (PwPrep), from
+// its shadow (or the blank world at op 0): the same pwf_reset_op sequence,
+// Philox slots and draws as an in-line auto-reset of episode S.episode + 1.
+// S.episode / S.ctrl are read while the main stream may be stepping (a
+// stale episode gives a shadow for an episode that never comes: not used).
+template <int WS>
+__global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_eu(kPwfWaves))) pwf_prepare_kernel(
+    const PowderParams* __restrict__ Pp, PowderState S, PwPrep prep, int32_t ops, uint32_t k0, uint32_t k1,
+    uint32_t r0, uint32_t r1) {
+  constexpr int C = WS * WS;
+  __shared__ PwFullShared<WS> sh;
+  const int64_t e = blockIdx.x;
+  const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;
+  const uint32_t target = __builtin_amdgcn_readfirstlane(S.episode[e]) + 1u;
+  int task = (__builtin_amdgcn_readfirstlane(S.ctrl[e]) >> 16) & 255;
+  if (task < 1 || task > Pp->num_tasks) task = 1;
+  const int len = Pp->seq_len[task - 1];
+  int q = (prep.tag[e] == prep.epoch && prep.ep[e] == target && prep.task[e] == task) ? prep.q[e] : 0;
+  q = __builtin_amdgcn_readfirstlane(q);
+  if (q > len) return;  // complete (uniform over the workgroup)
+  FW<WS> fw(sh);
+#ifdef OGBX_PWF_RULE_STAMPS
+  fw.diag_env = e;
+#endif
+  pwf_tables(sh, Pp);
+  if (q > 0) {
+    fw.load(prep.world + (size_t)e * C, prep.mom + (size_t)e * C, prep.vel + (size_t)e * C);
+    __syncthreads();
+  }
+  const int ne = Pp->num_elems, xy = Pp->xy_size;
+  const int re = (int)pw_draw(ge, target, 1, k0, k1, (uint32_t)ne);
+  const int rx = (int)pw_draw(ge, target, 2, k0, k1, (uint32_t)xy);
+  const int ry = (int)pw_draw(ge, target, 3, k0, k1, (uint32_t)xy);
+  for (int j = 0; j < ops && q <= len; ++j, ++q)
+    pwf_reset_op(fw, Pp, task, q, re, rx, ry, nullptr, r0, r1, ge, target, nullptr);
+  if (q > len) {
+#pragma unroll
+    for (int k = 0; k < FW<WS>::CPT; ++k) prep.goal[(size_t)e * C + fw.cell(k)] = sh.g[fw.cell(k)];
+  }
+  fw.store(prep.world + (size_t)e * C, prep.mom + (size_t)e * C, prep.vel + (size_t)e * C);
+  if (threadIdx.x == 0) {
+    prep.q[e] = q;
+    prep.ep[e] = target;
+    prep.task[e] = task;
+    prep.tag[e] = prep.epoch;
+  }
+}
+
 // k_steps env steps; rand: [k, N, 3, H, W] injected fields for the forward of
 // each third step, or NULL = Philox (auto-resets always use Philox).
 
@@ -668,7 +740,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     float* __restrict__ reward, uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated,
     uint8_t* __restrict__ success, int32_t auto_reset, uint32_t k0, uint32_t k1, uint32_t a0, uint32_t a1,
     uint32_t r0, uint32_t r1, const uint8_t* __restrict__ skip, int32_t refresh, int32_t chunk,
-    const int32_t* __restrict__ order, uint32_t* __restrict__ cost) {
+    const int32_t* __restrict__ order, uint32_t* __restrict__ cost, PwPrep prep) {
   constexpr int C = WS * WS, CPT = FW<WS>::CPT;
   __shared__ PwFullShared<WS> sh;
   FW<WS> fw(sh);
@@ -740,7 +812,7 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
     // one inlined forward)
     int op = fw_step ? -1 : 0, op_end = fw_step ? -1 : -2;
     int re = 0, rx = 0, ry = 0;
-    bool reset = false;
+    bool reset = false, shadow = false;
     auto finish_step = [&]() {
       if (threadIdx.x == 0) {
         reward[o] = succ ? 1.0f : 0.0f;
@@ -751,10 +823,16 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
       if (auto_reset && (succ || trunc)) {
         reset = true;
         ep += 1u;
-        re = (int)pw_draw(ge, ep, 1, k0, k1, (uint32_t)ne);
-        rx = (int)pw_draw(ge, ep, 2, k0, k1, (uint32_t)xy);
-        ry = (int)pw_draw(ge, ep, 3, k0, k1, (uint32_t)xy);
-        op_end = len;
+        // the episode's reset state prepared ahead (PwPrep), else in line
+        shadow = prep.use && prep.tag[e] == prep.epoch && prep.ep[e] == ep && prep.task[e] == task &&
+                 prep.q[e] > len;
+        shadow = __builtin_amdgcn_readfirstlane((int)shadow) != 0;
+        if (!shadow) {
+          re = (int)pw_draw(ge, ep, 1, k0, k1, (uint32_t)ne);
+          rx = (int)pw_draw(ge, ep, 2, k0, k1, (uint32_t)xy);
+          ry = (int)pw_draw(ge, ep, 3, k0, k1, (uint32_t)xy);
+          op_end = len;
+        }
       }
     };
     if (!fw_step) finish_step();
@@ -769,6 +847,13 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
       } else {
         pwf_reset_op(fw, Pp, task, op, re, rx, ry, nullptr, r0, r1, ge, ep, nullptr);
       }
+    }
+    if (shadow) {
+      __syncthreads();  // every lane is past its last read of the stepped world
+      fw.load(prep.world + (size_t)e * C, prep.mom + (size_t)e * C, prep.vel + (size_t)e * C);
+#pragma unroll
+      for (int kk = 0; kk < CPT; ++kk) sh.g[fw.cell(kk)] = prep.goal[(size_t)e * C + fw.cell(kk)];
+      __syncthreads();
     }
     if (reset) {
       succ = fw.errors() < tol;
@@ -1212,6 +1297,14 @@ struct ogbx_powder_env {
   int64_t phase = -1;
   uint64_t seed = 0;
   bool was_reset = false;
+  // next-episode reset states prepared ahead on a low-priority side stream
+  // (PwPrep; medium / hard, in-phase envs with auto-reset)
+  int32_t prep_ops = 0;           // replay ops per prepare launch (0: off, the default; OGBX_PWF_PREP_OPS)
+  ogbx::PwPrep prep{};            // device buffers + the current epoch
+  hipStream_t side = nullptr;     // created on first use, lowest priority
+  hipEvent_t ev_fork = nullptr, ev_side = nullptr;
+  int64_t prep_launched = 0;      // replay ops launched for the coming synchronized reset
+  bool side_pending = false;      // a prepare launch not yet joined
 };
 
 using namespace ogbx;
@@ -1229,6 +1322,15 @@ constexpr auto pwf_step_kernel_sparse = pwf_step_kernel<WS, true>;
     else                                                                                       \
       hipLaunchKernelGGL(kern<32>, dim3(grid), dim3(pwf_nt<32>()), 0, (hipStream_t)(stream), __VA_ARGS__); \
   } while (0)
+// Every prepared reset state so far is void (a reset or a new seed: the
+// Philox keys change): new epoch; in-flight prepare launches finish under the
+// old one, whose shadows are never used.  A caller's writes through the state
+// pointers need no epoch: a shadow is used only for the episode number and
+// task the env holds at its reset.
+inline void prep_invalidate(ogbx_powder_env* e) {
+  e->prep.epoch += 1u;
+  e->prep_launched = 0;
+}
 #define PW_LAUNCH(kern, e, grid, stream, ...)                                                  \
   do {                                                                                         \
     if ((e)->P.W == 64)                                                                        \
@@ -1345,6 +1447,24 @@ ogbx_status ogbx_powder_create(const ogbx_powder_opts* opts, int64_t n_envs, int
     if (h == hipSuccess) h = hipMalloc(&e->order, n * sizeof(int32_t));
     if (h == hipSuccess) h = hipMemset(e->cost, 0, n * sizeof(uint32_t));
     if (const char* v = std::getenv("OGBX_PWF_LIGHT")) e->light = std::atoi(v) != 0;  // A/B knob
+    if (const char* v = std::getenv("OGBX_PWF_PREP_OPS")) e->prep_ops = std::max(0, std::atoi(v));  // A/B knob
+    if (e->prep_ops > 0) {
+      if (h == hipSuccess) h = hipMalloc(&e->prep.world, n * HW);
+      if (h == hipSuccess) h = hipMalloc(&e->prep.mom, n * HW);
+      if (h == hipSuccess) h = hipMalloc(&e->prep.vel, n * HW * sizeof(float2));
+      if (h == hipSuccess) h = hipMalloc(&e->prep.goal, n * HW);
+      if (h == hipSuccess) h = hipMalloc(&e->prep.tag, n * sizeof(uint32_t));
+      if (h == hipSuccess) h = hipMalloc(&e->prep.ep, n * sizeof(uint32_t));
+      if (h == hipSuccess) h = hipMalloc(&e->prep.q, n * sizeof(int32_t));
+      if (h == hipSuccess) h = hipMalloc(&e->prep.task, n * sizeof(int32_t));
+      if (h == hipSuccess) h = hipMemset(e->prep.tag, 0, n * sizeof(uint32_t));
+      e->prep.epoch = 1;  // tag 0: never prepared
+      int least = 0, greatest = 0;
+      if (h == hipSuccess) h = hipDeviceGetStreamPriorityRange(&least, &greatest);
+      if (h == hipSuccess) h = hipStreamCreateWithPriority(&e->side, hipStreamNonBlocking, least);
+      if (h == hipSuccess) h = hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming);
+      if (h == hipSuccess) h = hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming);
+    }
     if (h == hipSuccess) h = hipMemset(e->S.mom, 0, n * HW);
     if (h == hipSuccess) h = hipMemset(e->S.vel, 0, n * HW * sizeof(float2));
     if (h == hipSuccess) h = hipMemset(e->S.goal_env, 0, n * HW);
@@ -1381,6 +1501,18 @@ ogbx_status ogbx_powder_destroy(ogbx_powder_t e) {
   (void)hipFree(e->handled);
   (void)hipFree(e->cost);
   (void)hipFree(e->order);
+  if (e->side) (void)hipStreamSynchronize(e->side);
+  (void)hipFree(e->prep.world);
+  (void)hipFree(e->prep.mom);
+  (void)hipFree(e->prep.vel);
+  (void)hipFree(e->prep.goal);
+  (void)hipFree(e->prep.tag);
+  (void)hipFree(e->prep.ep);
+  (void)hipFree(e->prep.q);
+  (void)hipFree(e->prep.task);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_side) (void)hipEventDestroy(e->ev_side);
+  if (e->side) (void)hipStreamDestroy(e->side);
   delete e;
   return OGBX_OK;
 }
@@ -1415,6 +1547,7 @@ ogbx_status ogbx_powder_reset(ogbx_powder_t e, const int32_t* task_id, const uin
              OGBX_EINVAL, "injected rand needs task_id, reset_action and rand_rows >= longest task + 1");
   OGBX_HIP(hipSetDevice(e->device));
   e->seed = seed;
+  prep_invalidate(e);
   uint32_t k0, k1, r0, r1;
   seed_key(seed, kTagPowderReset, &k0, &k1);
   seed_key(seed, kTagPowderRand, &r0, &r1);
@@ -1454,6 +1587,32 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
       all_full = j % 3 == 2 || (auto_reset && T > 0 && j + 1 >= T);
     }
     const bool light = e->light && k_steps == 1 && !all_full;
+    // prepared next-episode resets (PwPrep): in phase with auto-reset, one
+    // prepare launch of prep_ops replay ops on the side stream per render-only
+    // step until every env's reset is launched (the longest task: max_seq + 1
+    // ops); the synchronized reset step joins the side stream and loads them
+    const int64_t T = e->P.max_steps > 0 ? e->P.max_steps : 0;
+    const bool prep_on = e->prep_ops > 0 && e->side != nullptr && e->phase >= 0 && auto_reset && T > 0 &&
+                         k_steps == 1 && rand == nullptr && draws == nullptr;
+    ogbx::PwPrep prep = e->prep;
+    prep.use = 0;
+    bool sync_reset = false;
+    if (prep_on) {
+      const int64_t j = e->phase % T;
+      sync_reset = j + 1 >= T;
+      if (sync_reset && e->prep_launched >= e->max_seq + 1 && e->side_pending) {
+        OGBX_HIP(hipStreamWaitEvent((hipStream_t)stream, e->ev_side, 0));
+        e->side_pending = false;
+        prep.use = 1;
+      }
+    }
+    // fork before this render-only step's launches, so that the prepare may
+    // run beside them (it reads no state they write but ctrl's stage bits)
+    const bool prep_launch = prep_on && light && !sync_reset && e->prep_launched < e->max_seq + 1;
+    if (prep_launch) {
+      OGBX_HIP(hipEventRecord(e->ev_fork, (hipStream_t)stream));
+      OGBX_HIP(hipStreamWaitEvent(e->side, e->ev_fork, 0));
+    }
     if (light) {
       PW_LAUNCH(pwf_light_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, action, draws, obs, reward,
                 terminated, truncated, success, auto_reset, a0, a1, e->handled, (int32_t)e->cache_stale);
@@ -1464,7 +1623,8 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
       const int32_t chunk = kPwfSparseChunk;
       PWF_LAUNCH(pwf_step_kernel_sparse, e, (uint32_t)((e->n + chunk - 1) / chunk), stream, e->Pd, e->S, e->n,
                  action, draws, rand, k_steps, obs, reward, terminated, truncated, success, auto_reset, k0, k1, a0,
-                 a1, r0, r1, e->handled, (int32_t)e->cache_stale, chunk, (const int32_t*)nullptr, (uint32_t*)nullptr);
+                 a1, r0, r1, e->handled, (int32_t)e->cache_stale, chunk, (const int32_t*)nullptr, (uint32_t*)nullptr,
+                 prep);
     } else {
       // in-phase full step: workgroups longest first (the synchronized goal
       // replays by task length, forward steps by last measured cost)
@@ -1472,7 +1632,9 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
       if (all_full && e->n <= INT32_MAX) {
         const int64_t T = e->P.max_steps > 0 ? e->P.max_steps : 0;
         const int64_t j = (auto_reset && T > 0) ? e->phase % T : e->phase;
-        const int32_t by_task = (auto_reset && T > 0 && j + 1 >= T) ? 1 : 0;
+        // a synchronized reset step replays by task length, unless it loads
+        // prepared states (then the forward-cost order)
+        const int32_t by_task = (auto_reset && T > 0 && j + 1 >= T && !prep.use) ? 1 : 0;
         hipLaunchKernelGGL(pwf_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->Pd, e->S.ctrl, e->cost,
                            (int32_t)e->n, by_task, e->order);
         OGBX_LAUNCHED("pwf_order_kernel");
@@ -1480,9 +1642,21 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
       }
       PWF_LAUNCH(pwf_step_kernel_dense, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps,
                  obs, reward, terminated, truncated, success, auto_reset, k0, k1, a0, a1, r0, r1,
-                 light ? e->handled : (const uint8_t*)nullptr, (int32_t)e->cache_stale, 1, order, e->cost);
+                 light ? e->handled : (const uint8_t*)nullptr, (int32_t)e->cache_stale, 1, order, e->cost, prep);
     }
     OGBX_LAUNCHED("pwf_step_kernel");
+    if (sync_reset) e->prep_launched = 0;  // the next episode's round starts
+    if (prep_launch) {
+      uint32_t pk0, pk1, pr0, pr1;
+      seed_key(e->seed, kTagPowderReset, &pk0, &pk1);
+      seed_key(e->seed, kTagPowderRand, &pr0, &pr1);
+      PWF_LAUNCH(pwf_prepare_kernel, e, (uint32_t)e->n, e->side, e->Pd, e->S, e->prep, e->prep_ops, pk0, pk1, pr0,
+                 pr1);
+      OGBX_LAUNCHED("pwf_prepare_kernel");
+      OGBX_HIP(hipEventRecord(e->ev_side, e->side));
+      e->side_pending = true;
+      e->prep_launched += e->prep_ops;
+    }
     e->cache_stale = false;  // every env's cache was written by one of the two kernels
     if (e->phase >= 0) e->phase += k_steps;
   } else {
@@ -1534,6 +1708,7 @@ ogbx_status ogbx_powder_set_phase(ogbx_powder_t e, int64_t phase) {
 
 ogbx_status ogbx_powder_set_seed(ogbx_powder_t e, uint64_t seed) {
   OGBX_CHECK(e, OGBX_EINVAL, "null handle");
+  prep_invalidate(e);
   e->seed = seed;
   return OGBX_OK;
 }

@@ -474,3 +474,40 @@ def test_wrong_phase_hint_matches_fused(gpu, ne, size, phase):
     sa, sb = a.state_dict(), b.state_dict()
     for k in ('world', 'ctrl', 'elapsed', 'episode', 'momentum', 'velocity', 'goal'):
         assert torch.equal(sa[k], sb[k]), k
+
+
+@pytest.mark.parametrize('ne', [5, 8])
+def test_prepared_resets_match_inline_replays(gpu, ne, monkeypatch):
+    """OGBX_PWF_PREP_OPS (off by default): next-episode reset
+    states prepared on the low-priority side stream and loaded by the
+    synchronized auto-reset step give exactly the in-line goal replays'
+    outputs and state, and the reset step loads instead of replaying."""
+    n, T, K = 8, 45, 100
+    monkeypatch.setenv('OGBX_PWF_PREP_OPS', '8')
+    a = _env(gpu, n, ne=ne, size=32, max_episode_steps=T, auto_reset=True)
+    monkeypatch.delenv('OGBX_PWF_PREP_OPS')
+    b = _env(gpu, n, ne=ne, size=32, max_episode_steps=T, auto_reset=True)
+    opts = dict(task_id=torch.arange(n, device=gpu) % 5 + 1)
+    a.reset(seed=11, options=opts)
+    b.reset(seed=11, options=opts)
+    rng = np.random.RandomState(2)
+    acts = torch.tensor(rng.randint(0, max(ne, a._xy_action_size), size=(K, n)), dtype=torch.int32, device=gpu)
+    ms = {}
+    for t in range(K):
+        outs = {}
+        for name, env in (('a', a), ('b', b)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ob, rew, term, trunc, info = env.step(acts[t])
+            e1.record()
+            outs[name] = [x.clone() for x in (ob, rew, term, trunc, info['success'])]
+            if t == T - 1:
+                torch.cuda.synchronize()
+                ms[name] = e0.elapsed_time(e1)
+        for k, (x, y) in enumerate(zip(outs['a'], outs['b'])):
+            assert torch.equal(x, y), (t, k)
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in ('world', 'ctrl', 'elapsed', 'episode', 'momentum', 'velocity', 'goal'):
+        assert torch.equal(sa[k], sb[k]), k
+    # the synchronized reset at step T-1 loaded prepared states (no replay)
+    assert ms['a'] < ms['b'] / 3, ms
