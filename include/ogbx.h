@@ -172,7 +172,8 @@ ogbx_status ogbx_maze_step(ogbx_maze_t env, const void* action, int32_t action_i
  * Gymnasium surface returns the same tensors every step): bind the outputs
  * and the auto-reset flag once, then step with the action and the stream
  * only.  ogbx_maze_step_bound(env, a, f64, s) == ogbx_maze_step(env, a, f64, 1,
- * <bound outputs>, s); a new bind replaces the old one. */
+ * <bound outputs>, s); a new bind replaces the old one.  Ant handles bind the
+ * same way (obs f64[N,29]) for ogbx_antmaze_step_bound (below). */
 ogbx_status ogbx_maze_bind_step(ogbx_maze_t env, double* obs, float* reward, uint8_t* terminated,
                                 uint8_t* truncated, uint8_t* success, double* final_obs, int32_t auto_reset);
 ogbx_status ogbx_maze_step_bound(ogbx_maze_t env, const void* action, int32_t action_is_f64, void* stream);
@@ -227,6 +228,10 @@ ogbx_status ogbx_antmaze_step(ogbx_maze_t env, const double* qpos_post, const do
                               double* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
                               uint8_t* success, double* final_obs, int32_t auto_reset,
                               const double* reset_states, void* stream);
+/* ogbx_antmaze_step with the outputs and auto-reset flag of the last
+ * ogbx_maze_bind_step (the steady per-step call: four arguments). */
+ogbx_status ogbx_antmaze_step_bound(ogbx_maze_t env, const double* qpos_post, const double* qvel_post,
+                                    const double* reset_states, void* stream);
 
 /* Evaluation rollout without auto-reset: env i steps with actions device
  * [k_steps, N, 2] until the first step that ends its episode (terminated |

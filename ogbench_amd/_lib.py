@@ -81,6 +81,7 @@ _SIGNATURES = {
     ),
     'ogbx_maze_bind_step': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32]),
     'ogbx_maze_step_bound': (c_int32, [c_void_p, c_void_p, c_int32, c_void_p]),
+    'ogbx_antmaze_step_bound': (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     'ogbx_antmaze_state': (c_int32, [c_void_p, P(c_void_p), P(c_void_p)]),
     'ogbx_antmaze_reset': (
         c_int32,

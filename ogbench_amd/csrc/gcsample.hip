@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <mutex>
+#include <type_traits>
 
 #include "common.h"
 
@@ -26,9 +27,17 @@ namespace ogbx {
 constexpr int kGcMaxTile = 64;
 constexpr int kGcMaxCols = 32;
 
-struct GcColumns {
-  ogbx_gc_column c[kGcMaxCols];
+template <int N>
+struct GcColumnsN {
+  ogbx_gc_column c[N];
 };
+using GcColumns = GcColumnsN<kGcMaxCols>;
+// A sampler plan's batches of at most 16 columns (GC 9, HGC 15) launch with
+// this half-size table: the host's launch cost grows with the kernel
+// arguments (a 1,376-byte argument 2.5 -> 3.4 us per launch on ROCm 7,
+// profiles/r06_launch_host.txt), and a steady sample(1024) call is host-bound.
+constexpr int kGcSmallCols = 16;
+using GcColumnsSmall = GcColumnsN<kGcSmallCols>;
 
 __device__ inline uint64_t bounded64(uint32_t hi, uint32_t lo, uint64_t n) {
   const uint64_t u = ((uint64_t)hi << 32) | lo;
@@ -170,8 +179,8 @@ __device__ inline void copy_rows(const ogbx_gc_column& col, const int64_t* sel, 
 // kNt: non-temporal stores on the small-tile path (the HGC hit kernel: its 3.6
 // MB of rows per launch leave less to the end-of-kernel write-back, 6.44 ->
 // 6.34 us; GC's 1.3 MB measured 4.34 -> 4.38 us and keeps plain stores)
-template <int kSel, bool kNt = false>
-__device__ inline void copy_tile(const GcColumns& cols, int num_cols, const int64_t (*sel)[kGcMaxTile], int64_t base,
+template <int kSel, bool kNt = false, class Cols = GcColumns>
+__device__ inline void copy_tile(const Cols& cols, int num_cols, const int64_t (*sel)[kGcMaxTile], int64_t base,
                                  int n_here, bool flat4, int wave0 = 0) {
   if ((int)(threadIdx.x >> 6) < wave0) return;
   if (flat4) {
@@ -430,9 +439,9 @@ __device__ inline GcPick gc_wave_chain(const ogbx_gc_buffer& buf, const ogbx_gc_
 constexpr int kGcAheadWords = OGBX_GC_AHEAD_WORDS;
 constexpr int64_t kGcAheadMaxSamples = 1024;
 
-template <bool kHit>
+template <bool kHit, class Cols = GcColumns>
 __global__ void __launch_bounds__(256) gc_ahead_kernel(
-    ogbx_gc_buffer buf, ogbx_gc_config cfg, GcColumns cols, int32_t num_cols, uint32_t k0, uint32_t k1,
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, Cols cols, int32_t num_cols, uint32_t k0, uint32_t k1,
     uint32_t call_lo, uint32_t call_hi, uint32_t next_lo, uint32_t next_hi, double v_log_q, double a_log_q,
     const int64_t* __restrict__ ahead_in, int64_t* __restrict__ ahead_out, int64_t* idxs_out, int64_t* vgoal_out,
     int64_t* agoal_out, double* masks, double* rewards, bool flat4) {
@@ -814,9 +823,9 @@ constexpr int kHgcAheadWords = OGBX_HGC_AHEAD_WORDS;
 static_assert(kHgcAheadWords >= kHgcSel + 9, "HGC look-ahead record: 10 selectors + 9 scalars");
 
 // HGCDataset.sample with look-ahead (gc_ahead_kernel's scheme).
-template <bool kHit>
+template <bool kHit, class Cols = GcColumns>
 __global__ void __launch_bounds__(256) hgc_ahead_kernel(
-    ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, GcColumns cols, int32_t num_cols, uint32_t k0,
+    ogbx_gc_buffer buf, ogbx_gc_config cfg, ogbx_hgc_config hc, Cols cols, int32_t num_cols, uint32_t k0,
     uint32_t k1, uint32_t call_lo, uint32_t call_hi, uint32_t next_lo, uint32_t next_hi, double v_log_q,
     double a_log_q, double l_log_q, const int64_t* __restrict__ ahead_in, int64_t* __restrict__ ahead_out,
     ogbx_hgc_outputs o, bool flat4) {
@@ -1166,6 +1175,8 @@ struct PlanBatch {
   double *masks = nullptr, *rewards = nullptr;
   ogbx_hgc_outputs hout{};
   bool flat4 = false;
+  bool small = false;  // ncols <= kGcSmallCols: launch with cs
+  GcColumnsSmall cs{};
 };
 
 struct PlanPair {
@@ -1271,6 +1282,8 @@ ogbx_status ogbx_gc_plan_set_batch(ogbx_gc_plan_t p, int32_t slot, const ogbx_gc
   b.rewards = rewards;
   if (hgc_out) b.hout = *hgc_out;
   b.flat4 = flat4_columns(b.cc, num_cols);
+  b.small = num_cols <= kGcSmallCols;
+  for (int i = 0; i < kGcSmallCols && i < num_cols; ++i) b.cs.c[i] = b.cc.c[i];
   b.set = true;
   std::lock_guard<std::mutex> guard(p->mu);
   p->slots[slot] = b;
@@ -1341,19 +1354,25 @@ ogbx_status ogbx_gc_plan_sample(ogbx_gc_plan_t p, int32_t slot, uint64_t call_in
     out = p->pairs[pi].buf[which];
   }
   const uint64_t next = call_index + 1;
-  if (p->hgc) {
-    const auto kern = in ? hgc_ahead_kernel<true> : hgc_ahead_kernel<false>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, p->hcfg, b.cc,
-                       b.ncols, p->k0, p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q,
-                       p->a_log_q, p->l_log_q, in, out, b.hout, b.flat4);
-    OGBX_LAUNCHED("hgc_ahead_kernel");
-  } else {
-    const auto kern = in ? gc_ahead_kernel<true> : gc_ahead_kernel<false>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, b.cc, b.ncols,
-                       p->k0, p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q, p->a_log_q, in,
-                       out, b.idxs, b.vg, b.ag, b.masks, b.rewards, b.flat4);
-    OGBX_LAUNCHED("gc_ahead_kernel");
-  }
+  auto launch = [&](const auto& cols) {
+    using C = std::decay_t<decltype(cols)>;
+    if (p->hgc) {
+      const auto kern = in ? hgc_ahead_kernel<true, C> : hgc_ahead_kernel<false, C>;
+      hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, p->hcfg, cols, b.ncols, p->k0,
+                         p->k1, clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q, p->a_log_q, p->l_log_q,
+                         in, out, b.hout, b.flat4);
+    } else {
+      const auto kern = in ? gc_ahead_kernel<true, C> : gc_ahead_kernel<false, C>;
+      hipLaunchKernelGGL(kern, dim3((uint32_t)total), dim3(256), 0, s, p->buf, p->cfg, cols, b.ncols, p->k0, p->k1,
+                         clo, chi, (uint32_t)next, (uint32_t)(next >> 32), p->v_log_q, p->a_log_q, in, out, b.idxs,
+                         b.vg, b.ag, b.masks, b.rewards, b.flat4);
+    }
+  };
+  if (b.small)
+    launch(b.cs);
+  else
+    launch(b.cc);
+  OGBX_LAUNCHED(p->hgc ? "hgc_ahead_kernel" : "gc_ahead_kernel");
   p->key_valid = pi >= 0;
   p->key_pair = pi;
   p->key_which = which;

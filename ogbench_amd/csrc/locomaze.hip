@@ -970,8 +970,8 @@ ogbx_status ogbx_maze_step(ogbx_maze_t e, const void* action, int32_t action_is_
 ogbx_status ogbx_maze_bind_step(ogbx_maze_t e, double* obs, float* reward, uint8_t* terminated, uint8_t* truncated,
                                 uint8_t* success, double* final_obs, int32_t auto_reset) {
   OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
-  OGBX_CHECK(e->P.loco_type == 0, OGBX_EINVAL,
-             "only the point-mass dynamics are implemented (ant/humanoid are wrapper-only)");
+  OGBX_CHECK(e->P.loco_type == 0 || e->P.loco_type == 1, OGBX_EINVAL,
+             "ogbx_maze_bind_step: point handles (ogbx_maze_step_bound) or ant handles (ogbx_antmaze_step_bound)");
   OGBX_CHECK(obs && reward && terminated && truncated && success, OGBX_EINVAL, "ogbx_maze_bind_step: null output");
   e->b_obs = obs;
   e->b_reward = reward;
@@ -986,6 +986,8 @@ ogbx_status ogbx_maze_bind_step(ogbx_maze_t e, double* obs, float* reward, uint8
 
 ogbx_status ogbx_maze_step_bound(ogbx_maze_t e, const void* action, int32_t action_is_f64, void* stream) {
   OGBX_CHECK(e != nullptr && action != nullptr, OGBX_EINVAL, "ogbx_maze_step_bound: null argument");
+  OGBX_CHECK(e->P.loco_type == 0, OGBX_EINVAL,
+             "only the point-mass dynamics are implemented (ant/humanoid are wrapper-only)");
   OGBX_CHECK(e->bound, OGBX_ESTATE, "ogbx_maze_step_bound: no outputs bound (ogbx_maze_bind_step)");
   OGBX_CHECK(e->was_reset, OGBX_ESTATE, "Cannot call env.step() before calling env.reset()");
   return maze_step_launch(e, action, action_is_f64, 1, e->b_obs, e->b_reward, e->b_term, e->b_trunc, e->b_succ,
@@ -1016,6 +1018,14 @@ ogbx_status ogbx_antmaze_reset(ogbx_maze_t e, const int32_t* task_id, const doub
   OGBX_LAUNCHED("ant_reset_kernel");
   e->was_reset = true;
   return OGBX_OK;
+}
+
+ogbx_status ogbx_antmaze_step_bound(ogbx_maze_t e, const double* qpos_post, const double* qvel_post,
+                                    const double* reset_states, void* stream) {
+  OGBX_CHECK(e != nullptr, OGBX_EINVAL, "null handle");
+  OGBX_CHECK(e->bound, OGBX_ESTATE, "ogbx_antmaze_step_bound: no outputs bound (ogbx_maze_bind_step)");
+  return ogbx_antmaze_step(e, qpos_post, qvel_post, e->b_obs, e->b_reward, e->b_term, e->b_trunc, e->b_succ,
+                           e->b_final, e->b_auto, reset_states, stream);
 }
 
 ogbx_status ogbx_antmaze_step(ogbx_maze_t e, const double* qpos_post, const double* qvel_post, double* obs,

@@ -573,35 +573,45 @@ __device__ __forceinline__ double kp_or_far(bool on, double kp) {
 // (a_e the edge activities; PieceWeights carries A2 = a0+a1+a2 and C2 = a2).
 __device__ __forceinline__ void local_piece_min(const LocalSlots& c, const PieceWeights& p, double vx, double vy,
                                                 double* ux, double* uy) {
-#pragma clang fp contract(fast)
+  // Every fused multiply-add is written out (no contraction pragma here or in
+  // local_corner_res): the solve has three call sites -- the stage's solve,
+  // the first stage's Newton step and the active-set iterations -- and the
+  // iterations' trip count is wave-uniform, so a lane that settled before them
+  // reruns the solve at another site.  With contraction left to the compiler
+  // the sites fused differently, the rerun differed by 1 ulp, and a lane's
+  // result depended on whether another lane of its wave iterated (round 6,
+  // scripts/probe_epw_diff.py at 8 envs per wave).  The fusion written here
+  // is the compiler's choice at the stage's own site; restoring the settled
+  // lanes' values after the loop instead measured 2-7 % slower (register and
+  // layout effects on the hot path).
   const double w0 = c.w0, w1 = c.w1, w2 = c.w2;
   const double nx = c.nx2, ny = c.ny2;
   const double c2 = fma(nx, nx, -(ny * ny)), s2 = (nx + nx) * ny;
   const double A = w2 * p.A2, B = w2 * p.D2, C = w2 * p.C2;  // B = -(a1 - a0) w2
   const double X = fma(C, c2, -(B * s2));
-  const double mpA = c.mp + A;
-  double h00 = fma(w0, p.S0, fma(w1, p.T1, mpA)) + X;
-  double h11 = fma(w0, p.T0, fma(w1, p.S1, mpA)) - X;
+  const double mpA = fma(w2, p.A2, c.mp);  // = c.mp + A
+  const double h00 = fma(w0, p.S0, fma(w1, p.T1, mpA)) + X;
+  const double h11 = fma(w0, p.T0, fma(w1, p.S1, mpA)) - X;
   double h01 = fma(w0, p.D0, -(w1 * p.D1));
   h01 = fma(C, s2, h01);
   h01 = fma(B, c2, h01);
   const double g0 = w0 * c.kp0, g1 = w1 * c.kp1;
-  double r0 = c.mbp * vx + g0 * p.S0 - g1 * p.D1;
-  double r1 = c.mbp * vy + g0 * p.D0 + g1 * p.S1;
-  const double WS = A + C, k2 = c.kp2;
-  r0 -= k2 * (WS * nx - B * ny);
-  r1 -= k2 * (WS * ny + B * nx);
-  const double idet = fast_recip(h00 * h11 - h01 * h01);
-  *ux = (h11 * r0 - h01 * r1) * idet;
-  *uy = (h00 * r1 - h01 * r0) * idet;
+  double r0 = fma(-g1, p.D1, fma(g0, p.S0, c.mbp * vx));
+  double r1 = fma(g1, p.S1, fma(g0, p.D0, c.mbp * vy));
+  const double WS = fma(w2, p.C2, A), k2 = c.kp2;  // = A + C
+  r0 = fma(-k2, fma(WS, nx, -(B * ny)), r0);
+  r1 = fma(-k2, fma(WS, ny, B * nx), r1);
+  const double idet = fast_recip(fma(h00, h11, -(h01 * h01)));
+  *ux = fma(h11, r0, -(h01 * r1)) * idet;
+  *uy = fma(h00, r1, -(h01 * r0)) * idet;
 }
 
 // The corner slot's residual pair (a = n.u + kp, b = t.u) at U: one
-// definition for the mask and the settled test, so both see the same values.
+// definition for the mask and the settled test, so both see the same values
+// (fused explicitly, as local_piece_min).
 __device__ __forceinline__ void local_corner_res(const LocalSlots& c, double ux, double uy, double* a, double* b) {
-#pragma clang fp contract(fast)
-  *a = c.nx2 * ux + (c.ny2 * uy + c.kp2);
-  *b = c.nx2 * uy - c.ny2 * ux;
+  *a = fma(c.nx2, ux, fma(c.ny2, uy, c.kp2));
+  *b = fma(c.nx2, uy, -(c.ny2 * ux));
 }
 
 // Active-edge mask at U (local role layout, bits as edge_mask).
@@ -763,9 +773,9 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
       // chain about twice as slowly with <= 8 active lanes, so
       // the divergent per-lane loop ran at half speed (round 5 A/B: 12.10 ->
       // 11.54 us per launch at N = 65,536, 10.79 -> 10.40 at 8,192).  A
-      // settled lane is at a fixed point (act == A2, pw = piece_weights(act))
-      // and keeps its settled values, so every lane's result equals the
-      // per-lane loop's.
+      // settled lane is at a fixed point (act == A2, pw = piece_weights(act)):
+      // its rerun recomputes the same ux, uy and A2 bit for bit, so every
+      // lane's result equals the per-lane loop's.
 #pragma unroll 1
       for (int it = 0; it < kLeanIters; ++it) {
         OGBX_WPATH(20);
@@ -777,21 +787,10 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
         if (!done) OGBX_STAT(4);
         trips += !done;
 #endif
-        // A settled lane keeps the values it settled with: the rerun would
-        // recompute them at another call site, which the compiler may fuse
-        // differently (1 ulp: round 6, scripts/probe_epw_diff.py at 8 envs
-        // per wave), and its result would then depend on whether another
-        // lane of its wave iterates.  Two selects in the cold loop only.
-        const bool settled = done;
-        const double ux0 = ux, uy0 = uy;
-        const uint32_t A20 = A2;
         act = A2;
         piece_weights(act, pw);
         local_piece_min(c, pw, vsx, vsy, &ux, &uy);
         A2 = local_edge_mask(c, ux, uy);
-        ux = settled ? ux0 : ux;
-        uy = settled ? uy0 : uy;
-        A2 = settled ? A20 : A2;
         done = A2 == act;
         if (!__any(!done)) break;
       }

@@ -368,6 +368,11 @@ class GCDataset:
         # state live in libogbx, so a steady call is one lookup and one launch
         self._lookahead = bool(config.get('lookahead', self._LOOKAHEAD_DEFAULT))
         self._p_aug = config.get('p_aug')
+        # the reference draws np.random.rand() < p_aug per call (datasets.py:278);
+        # with p_aug 0 the test can never pass and the draw would only advance
+        # numpy's global stream (which this sampler's Philox draws do not
+        # follow), so the steady call skips it
+        self._p_aug_live = self._p_aug is not None and float(self._p_aug) > 0.0
         self._dev_idx = self.device.index
         self._plan_sample = L.ogbx_gc_plan_sample
         self._raw_stream = torch._C._cuda_getCurrentRawStream  # hipStream_t of the current stream, as an int
@@ -436,7 +441,7 @@ class GCDataset:
         if (gen is not None and gen == self._rec_gen) or \
                 all(map(operator.is_, map(ds.get, self._rec_keys), self._rec_tensors)):
             if tuple(map(_VERSION, self._rec_tensors)) == self._rec_versions:
-                self._rec_gen = gen
+                self._rec_gen = gen  # verified: the next calls compare the generation only
                 return
         stale = False
         for k, t, _, _, ver in self._rec_src:
@@ -561,7 +566,13 @@ class GCDataset:
         """
         plain_call = idxs is None and not draws and not record_draws and _keys is None
         if self._rec_src:
-            self._refresh_record()
+            # staleness of the packed row record: a Dataset's generation (no
+            # column replaced since the last verified check) and the packed
+            # columns' version counters; anything else takes the full check
+            gen = getattr(self.dataset, '_gen', None)
+            if (gen is None or gen != self._rec_gen
+                    or tuple(map(_VERSION, self._rec_tensors)) != self._rec_versions):
+                self._refresh_record()
         if out is not None and plain_call:
             # the steady refill: one dict lookup, one ctypes call (host time
             # per call is what bounds sample(1024)'s rate, bench 'extra')
@@ -573,7 +584,7 @@ class GCDataset:
                 st = self._plan_sample(self._plan, hit[2], call, self._raw_stream(self._dev_idx))
                 if st:
                     _lib.check(st, 'gc_sample')
-                if self._p_aug is not None and not evaluation:
+                if self._p_aug_live and not evaluation:
                     self._p_aug_draw(out, evaluation)
                 return out
         torch = _torch()
@@ -801,7 +812,13 @@ class HGCDataset(GCDataset):
         total = int(batch_size) * int(num_batches)
         plain_call = idxs is None and not draws and not record_draws
         if self._rec_src:
-            self._refresh_record()
+            # staleness of the packed row record: a Dataset's generation (no
+            # column replaced since the last verified check) and the packed
+            # columns' version counters; anything else takes the full check
+            gen = getattr(self.dataset, '_gen', None)
+            if (gen is None or gen != self._rec_gen
+                    or tuple(map(_VERSION, self._rec_tensors)) != self._rec_versions):
+                self._refresh_record()
         hit = self._out_cache.get(id(out)) if (out is not None and plain_call) else None
         if (hit is not None and hit[0] is out and hit[1] == (batch_size, num_batches)
                 and self._plan_seed == self._seed):
@@ -810,7 +827,7 @@ class HGCDataset(GCDataset):
             st = self._plan_sample(self._plan, hit[2], call, self._raw_stream(self._dev_idx))
             if st:
                 _lib.check(st, 'hgc_sample')
-            if self._p_aug is not None and not evaluation:
+            if self._p_aug_live and not evaluation:
                 self._p_aug_draw(out, evaluation)
             return out
         else:

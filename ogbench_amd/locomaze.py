@@ -141,6 +141,7 @@ class MazeEnv:
         self._h = h
         self._L = L
         self._wrap_fn = L.ogbx_antmaze_step
+        self._wrap_bound = L.ogbx_antmaze_step_bound
 
         self.maze_map, tasks = static_tables(maze_type)
         self.task_infos = []
@@ -570,7 +571,11 @@ class MazeEnv:
             qp, vp = hit[2], hit[3]
         else:
             qp, vp = self._wrap_validate(qpos, qvel)
-        st = self._wrap_fn(self._h, qp, vp, *self._step_out, self._auto_i, rs, _raw_stream(self._dev_idx))
+        auto = self._auto_i
+        if auto != self._bound_auto:
+            _lib.check(self._L.ogbx_maze_bind_step(self._h, *self._step_out, auto), 'wrap_step')
+            self._bound_auto = auto
+        st = self._wrap_bound(self._h, qp, vp, rs, _raw_stream(self._dev_idx))
         if st != 0:
             _lib.check(st, 'wrap_step')
         info = {'success': self._succ_b}

@@ -50,6 +50,7 @@ def main():
     ap.add_argument('--round', required=True)
     ap.add_argument('--workload', required=True)
     ap.add_argument('--kernel', required=True)
+    ap.add_argument('--label', default=None, help="traffic.json key's kernel name (default: --kernel), as bench.py names it")
     ap.add_argument('--units', type=int, required=True, help='envs or samples per launch of the profiled run')
     ap.add_argument('--world', type=int, default=1)
     ap.add_argument('--out', default=os.path.join(ROOT, 'gpurun_out'))
@@ -102,7 +103,7 @@ def main():
         with open(tpath) as f:
             data = json.load(f)
     # keyed by workload; bench.py uses it only for a run of the same units and world size
-    data[f'{a.kernel}@{a.workload}'] = rec
+    data[f'{a.label or a.kernel}@{a.workload}'] = rec
     with open(tpath, 'w') as f:
         json.dump(data, f, indent=1, sort_keys=True)
     print(json.dumps({a.kernel: rec}))

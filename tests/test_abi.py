@@ -34,7 +34,7 @@ ABI5_SYMBOLS = {
     'ogbx_maze_describe', 'ogbx_maze_tables', 'ogbx_maze_static_tables', 'ogbx_maze_reset', 'ogbx_maze_step', 'ogbx_maze_bind_step', 'ogbx_maze_step_bound',
     'ogbx_maze_rollout_until_done', 'ogbx_maze_state', 'ogbx_maze_set_seed', 'ogbx_point_physics',
     'ogbx_maze_xy_to_ij', 'ogbx_maze_ij_to_xy', 'ogbx_maze_oracle_subgoal', 'ogbx_maze_expert_action',
-    'ogbx_maze_set_goal', 'ogbx_antmaze_state', 'ogbx_antmaze_reset', 'ogbx_antmaze_step',
+    'ogbx_maze_set_goal', 'ogbx_antmaze_state', 'ogbx_antmaze_reset', 'ogbx_antmaze_step', 'ogbx_antmaze_step_bound',
     # powderworld
     'ogbx_powder_create', 'ogbx_powder_destroy', 'ogbx_powder_describe', 'ogbx_powder_goal_worlds',
     'ogbx_powder_reset', 'ogbx_powder_step', 'ogbx_powder_state', 'ogbx_powder_state_view',
