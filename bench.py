@@ -397,7 +397,13 @@ def _eval_allgather(env, world, dev, steps=1000):
                overall_success=m.get('evaluation/overall_success'), allgather_ms=ms,
                per_task={k.split('/')[1]: v for k, v in m.items() if k != 'evaluation/overall_success'})
     if world > 1:
-        res.update(_cabi_allgather_check(counters, per_rank, world, dev))
+        # the C-ABI communicator (a second RCCL communicator per rank) has no
+        # multi-GPU run on record yet: opt-in, so that an untried path cannot
+        # stall the scaling run
+        if os.environ.get('OGBX_BENCH_CABI_COMM') == '1':
+            res.update(_cabi_allgather_check(counters, per_rank, world, dev))
+        else:
+            res['cabi_allgather'] = 'not run (set OGBX_BENCH_CABI_COMM=1)'
     return res
 
 

@@ -845,6 +845,16 @@ ogbx_status ogbx_diag_wave_stamps(unsigned long long* out) {
 }
 #endif
 
+#ifdef OGBX_MASK_TRACE
+// Diagnostic build only: the lean stages' start / settled masks of the last
+// launch (point_contact.h g_mask_trace, 40 words per global thread).
+ogbx_status ogbx_diag_mask_trace(uint32_t* out) {
+  OGBX_HIP(hipDeviceSynchronize());
+  OGBX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mask_trace), 65536 * 40 * sizeof(uint32_t)));
+  return OGBX_OK;
+}
+#endif
+
 #ifdef OGBX_STAGE_STAMPS
 // Diagnostic build only: the per-wave lean-stage cycle parts of the last
 // launch (point_contact.h g_wave_stages, 8 words per wave), then cleared.

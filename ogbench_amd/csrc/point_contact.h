@@ -518,6 +518,13 @@ __device__ __forceinline__ double band_u(const PointModel& pm, double d) {
 __device__ unsigned long long g_wave_paths[4096];
 #endif
 
+#ifdef OGBX_MASK_TRACE
+// Diagnostic build only: per global thread (= env at 64 envs per wave) and
+// lean stage, the active-edge mask the stage started from and the one it
+// settled on (scripts/probe_mask_trace.py).
+__device__ uint32_t g_mask_trace[65536 * 40];
+#endif
+
 #ifdef OGBX_STAGE_STAMPS
 // Diagnostic build only: shader-clock cycles per part of the lean stage,
 // summed over the step's 20 stages, per wave (first active lane stores):
@@ -736,6 +743,10 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
     LeanHit k;
     if (more) local_collide(L, nex, ney, k, ehi);
     OGBX_SS_AT(ss0);
+#ifdef OGBX_MASK_TRACE
+    const uint32_t mt_tid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (mt_tid < 65536) g_mask_trace[mt_tid * 40 + 2 * e] = act;
+#endif
     double ux, uy;
     local_piece_min(c, pw, vsx, vsy, &ux, &uy);
     OGBX_SS_AT(ss1);
@@ -800,6 +811,9 @@ __device__ __forceinline__ void contact_loop_local(const PointModel& pm, double&
 #endif
     }
     OGBX_SS_AT(ss4);
+#ifdef OGBX_MASK_TRACE
+    if (mt_tid < 65536) g_mask_trace[mt_tid * 40 + 2 * e + 1] = act | (done ? 0u : 0x80000000u);
+#endif
     double fx, fy;
     {
 #pragma clang fp contract(fast)

@@ -1,10 +1,11 @@
 """The diagnostic build toggles still compile (CPU: hipcc cross-compiles gfx950).
 
-The shipped kernels carry exactly four compile-time toggles, all diagnostic
+The shipped kernels carry exactly five compile-time toggles, all diagnostic
 (they add counters or clock stamps and change no result):
   * OGBX_PHYS_STATS  -- contact-path counters (point_physics.h, point_contact.h)
   * OGBX_WAVE_STAMPS -- per-wave wall-clock stamps + path counts (locomaze.hip)
   * OGBX_STAGE_STAMPS -- per-wave cycles of each part of the lean contact stage
+  * OGBX_MASK_TRACE  -- per-env start / settled active-edge masks of every lean stage
   * OGBX_PWF_RULE_STAMPS -- per-rule cycle stamps of the full powderworld forward
 No test builds them otherwise, so this one does (device code only, -O1 to keep
 the CPU suite short; the two source files compile in parallel).
@@ -25,7 +26,7 @@ FLAGS = ['-O1', '-std=c++17', '--offload-arch=gfx950', '-ffp-contract=off', '-Wa
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason='hipcc not installed')
 def test_diagnostic_toggles_compile(tmp_path):
     jobs = {
-        'locomaze': ['-DOGBX_PHYS_STATS', '-DOGBX_WAVE_STAMPS', '-DOGBX_STAGE_STAMPS'],
+        'locomaze': ['-DOGBX_PHYS_STATS', '-DOGBX_WAVE_STAMPS', '-DOGBX_STAGE_STAMPS', '-DOGBX_MASK_TRACE'],
         'powder': ['-DOGBX_PWF_RULE_STAMPS'],
     }
     procs = {}
@@ -42,7 +43,7 @@ def test_diagnostic_toggles_compile(tmp_path):
 
 def test_no_ab_toggles_left_in_kernels():
     """Only the diagnostic toggles remain: no compiled-out A/B variant code."""
-    allowed = {'OGBX_PHYS_STATS', 'OGBX_WAVE_STAMPS', 'OGBX_STAGE_STAMPS', 'OGBX_PWF_RULE_STAMPS'}
+    allowed = {'OGBX_PHYS_STATS', 'OGBX_WAVE_STAMPS', 'OGBX_STAGE_STAMPS', 'OGBX_MASK_TRACE', 'OGBX_PWF_RULE_STAMPS'}
     found = set()
     for name in os.listdir(CSRC):
         if not name.endswith(('.hip', '.h')):
