@@ -149,6 +149,20 @@ constexpr int kAntPer = (kAntEnvs * kAntOb + kAntThreads - 1) / kAntThreads;
 //   after one barrier the first wave overwrites the rows phase A changed:
 //     a teleport's body xy, an auto-reset's whole rows (rare).  The barrier
 //     orders those writes after the plain ones of the other waves.
+// kVec (every row pointer 16-byte aligned, the host checks): phase B moves
+// the block's qpos / qvel ranges as 16-byte words -- loads, and the body
+// state stores straight from them -- and assembles the obs rows in LDS,
+// stored as 16-byte words after the barrier; phase A runs before that
+// barrier and leaves each env's row kind in LDS, so the plain obs stores
+// skip the auto-reset rows and need no second barrier.
+typedef double AntD2 __attribute__((ext_vector_type(2)));
+// one 16-byte streaming store (p 16-byte aligned)
+__device__ __forceinline__ void ant_nt_store2(double* p, double2 v) {
+  const AntD2 w = {v.x, v.y};
+  __builtin_nontemporal_store(w, reinterpret_cast<AntD2*>(p));
+}
+
+template <bool kVec>
 __global__ void __launch_bounds__(kAntThreads) ant_step_kernel(
     const MazeParams* __restrict__ Pp, MazeState S, double* __restrict__ bq, double* __restrict__ bv, int64_t n,
     const double* __restrict__ qpost, const double* __restrict__ vpost, int32_t in_place,
@@ -166,12 +180,37 @@ __global__ void __launch_bounds__(kAntThreads) ant_step_kernel(
   double* bqb = bq + kAntNq * base;
   double* bvb = bv + kAntNv * base;
   double val[kAntPer];
+  // kVec: word j of the block's qpos (qvel) range holds elements 2j, 2j + 1
+  constexpr int kQW = (kAntEnvs * kAntNq / 2 + kAntThreads - 1) / kAntThreads;
+  constexpr int kVW = (kAntEnvs * kAntNv / 2 + kAntThreads - 1) / kAntThreads;
+  const int nq = nb * kAntNq, nv = nb * kAntNv;  // nv is even
+  double2 qw[kQW], vw[kVW];
+  __shared__ double rows[kAntEnvs * kAntOb];
+  __shared__ uint8_t kinds[kAntEnvs];
+  if constexpr (!kVec) {
 #pragma unroll
-  for (int r = 0; r < kAntPer; ++r) {
-    const int f = (int)threadIdx.x + kAntThreads * r;
-    const int e = f / kAntOb, c = f - e * kAntOb;
-    val[r] = 0.0;
-    if (f < tot) val[r] = c < kAntNq ? qb[kAntNq * e + c] : vb[kAntNv * e + (c - kAntNq)];
+    for (int r = 0; r < kAntPer; ++r) {
+      const int f = (int)threadIdx.x + kAntThreads * r;
+      const int e = f / kAntOb, c = f - e * kAntOb;
+      val[r] = 0.0;
+      if (f < tot) val[r] = c < kAntNq ? qb[kAntNq * e + c] : vb[kAntNv * e + (c - kAntNq)];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < kQW; ++r) {
+      const int j = (int)threadIdx.x + kAntThreads * r;
+      qw[r] = make_double2(0.0, 0.0);
+      if (2 * j + 1 < nq)
+        qw[r] = reinterpret_cast<const double2*>(qb)[j];
+      else if (2 * j < nq)
+        qw[r].x = qb[2 * j];
+    }
+#pragma unroll
+    for (int r = 0; r < kVW; ++r) {
+      const int j = (int)threadIdx.x + kAntThreads * r;
+      vw[r] = make_double2(0.0, 0.0);
+      if (2 * j < nv) vw[r] = reinterpret_cast<const double2*>(vb)[j];
+    }
   }
   const int64_t i = base + threadIdx.x;
   const bool lane_a = threadIdx.x < kAntEnvs && i < n;
@@ -190,7 +229,7 @@ __global__ void __launch_bounds__(kAntThreads) ant_step_kernel(
   }
   // phase B: the plain rows
 #pragma unroll
-  for (int r = 0; r < kAntPer; ++r) {
+  for (int r = 0; r < (kVec ? 0 : kAntPer); ++r) {
     const int f = (int)threadIdx.x + kAntThreads * r;
     if (f >= tot) continue;
     const int e = f / kAntOb, c = f - e * kAntOb;
@@ -234,7 +273,52 @@ __global__ void __launch_bounds__(kAntThreads) ant_step_kernel(
     success[i] = succ;
     if (auto_reset && (term || trunc)) kind = kRowReset;
   }
-  __syncthreads();  // the plain rows above are written before the overwrites below
+  if constexpr (kVec) {
+    // body state from the loaded words; obs rows assembled in LDS
+#pragma unroll
+    for (int r = 0; r < kQW; ++r) {
+      const int j = (int)threadIdx.x + kAntThreads * r;
+      if (2 * j >= nq) continue;
+      const bool two = 2 * j + 1 < nq;
+      if (!in_place) {
+        if (two)
+          ant_nt_store2(&bqb[2 * j], qw[r]);
+        else
+          __builtin_nontemporal_store(qw[r].x, &bqb[2 * j]);
+      }
+      const int e0 = (2 * j) / kAntNq, c0 = 2 * j - e0 * kAntNq;
+      rows[kAntOb * e0 + c0] = qw[r].x;
+      if (two) {
+        const int e1 = (2 * j + 1) / kAntNq, c1 = 2 * j + 1 - e1 * kAntNq;
+        rows[kAntOb * e1 + c1] = qw[r].y;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kVW; ++r) {
+      const int j = (int)threadIdx.x + kAntThreads * r;
+      if (2 * j >= nv) continue;
+      if (!in_place) ant_nt_store2(&bvb[2 * j], vw[r]);
+      const int e0 = (2 * j) / kAntNv, c0 = 2 * j - e0 * kAntNv;  // 2j, 2j + 1: one row (kAntNv even)
+      rows[kAntOb * e0 + kAntNq + c0] = vw[r].x;
+      rows[kAntOb * e0 + kAntNq + c0 + 1] = vw[r].y;
+    }
+    if (threadIdx.x < kAntEnvs) kinds[threadIdx.x] = kind;
+    __syncthreads();  // rows and kinds complete; the body stores above precede the overwrites below
+    // plain obs rows as 16-byte words (a word may span two rows: both must
+    // be plain; the auto-reset rows are written whole below)
+    for (int j = (int)threadIdx.x; 2 * j < tot; j += kAntThreads) {
+      const int e0 = (2 * j) / kAntOb, e1 = (2 * j + 1) / kAntOb;
+      const bool p0 = kinds[e0] != kRowReset, p1 = 2 * j + 1 < tot && kinds[e1] != kRowReset;
+      if (p0 && p1)
+        ant_nt_store2(&ob[2 * j], reinterpret_cast<const double2*>(rows)[j]);
+      else {
+        if (p0) __builtin_nontemporal_store(rows[2 * j], &ob[2 * j]);
+        if (p1) __builtin_nontemporal_store(rows[2 * j + 1], &ob[2 * j + 1]);
+      }
+    }
+  } else {
+    __syncthreads();  // the plain rows above are written before the overwrites below
+  }
   if (lane_a) {
     if (kind == kRowReset) {
       if (final_obs != nullptr) {  // the pre-reset observation

@@ -1051,9 +1051,14 @@ ogbx_status ogbx_antmaze_step(ogbx_maze_t e, const double* qpos_post, const doub
   OGBX_HIP(hipSetDevice(e->device));
   uint32_t k0, k1;
   seed_key(e->seed, kTagMazeReset, &k0, &k1);
-  hipLaunchKernelGGL(ant_step_kernel, dim3(grid_for(e->n, kAntEnvs)), dim3(kAntThreads), 0, (hipStream_t)stream, e->Pd, e->S,
-                     e->body_qpos, e->body_qvel, e->n, qpos_post, qvel_post, (int32_t)qin, obs, reward, terminated,
-                     truncated, success, final_obs, auto_reset, reset_states, k0, k1);
+  // 16-byte row words when every row pointer allows them
+  const bool vec = ((reinterpret_cast<uintptr_t>(qpos_post) | reinterpret_cast<uintptr_t>(qvel_post) |
+                     reinterpret_cast<uintptr_t>(obs) | reinterpret_cast<uintptr_t>(e->body_qpos) |
+                     reinterpret_cast<uintptr_t>(e->body_qvel)) & 15u) == 0;
+  hipLaunchKernelGGL(vec ? ant_step_kernel<true> : ant_step_kernel<false>, dim3(grid_for(e->n, kAntEnvs)),
+                     dim3(kAntThreads), 0, (hipStream_t)stream, e->Pd, e->S, e->body_qpos, e->body_qvel, e->n,
+                     qpos_post, qvel_post, (int32_t)qin, obs, reward, terminated, truncated, success, final_obs,
+                     auto_reset, reset_states, k0, k1);
   OGBX_LAUNCHED("ant_step_kernel");
   return OGBX_OK;
 }

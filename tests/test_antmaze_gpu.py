@@ -172,6 +172,45 @@ def test_teleport_moves_body_xy(gpu):
     assert np.array_equal(bq.cpu().numpy()[:, :2], xy)
 
 
+@pytest.mark.parametrize('n', [67, 129, 1000])
+def test_row_words_match_scalar_rows(gpu, n):
+    """The 16-byte row path (every row pointer 16-byte aligned) and the 8-byte
+    one (inputs offset by one double) give the same outputs, body state and
+    final observations, on ragged tail blocks (an odd number of envs: a word
+    that spans two rows, a lone last element) and with auto-reset rows mixed
+    among plain ones (envs placed on their goal terminate)."""
+    seed = 5
+    envs = [_env(gpu, n, 'post', auto_reset=True) for _ in range(2)]
+    for env in envs:
+        env.reset(seed=seed, options=dict(task_id=torch.tensor((np.arange(n) % 5 + 1).astype(np.int32))))
+    rng = np.random.RandomState(7)
+    q = rng.normal(size=(n, 15)) + 100.0
+    v = rng.normal(size=(n, 14))
+    on_goal = rng.rand(n) < 0.3
+    q[on_goal, :2] = envs[0].cur_goal_xy.cpu().numpy()[on_goal]
+    rs = rng.normal(size=(n, 29))
+    outs = []
+    for k, env in enumerate(envs):
+        qb = torch.zeros(n * 15 + 1, dtype=torch.float64, device=gpu)
+        vb = torch.zeros(n * 14 + 1, dtype=torch.float64, device=gpu)
+        qt = qb[k:k + n * 15].view(n, 15)
+        vt = vb[k:k + n * 14].view(n, 14)
+        assert (qt.data_ptr() % 16 == 0) == (k == 0)
+        qt.copy_(torch.tensor(q))
+        vt.copy_(torch.tensor(v))
+        o, r, te, tr, info = env.wrap_step(qt, vt, reset_states=torch.tensor(rs, device=gpu))
+        bq, bv = env.body_state()
+        outs.append([x.cpu().numpy().copy() for x in (o, r, te, tr, info['final_observation'], bq, bv)])
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    o, te = outs[0][0], outs[0][2]
+    assert np.array_equal(te, on_goal) and 0 < on_goal.sum() < n
+    plain = ~on_goal
+    assert np.array_equal(o[plain], np.concatenate([q, v], 1)[plain])
+    assert np.array_equal(o[on_goal][:, 2:], rs[on_goal][:, 2:])
+    assert np.array_equal(outs[0][5][plain], q[plain]) and np.array_equal(outs[0][6][plain], v[plain])
+
+
 def test_point_only_entry_points_refuse_ant(gpu):
     env = _env(gpu, 4, 'post')
     env.reset(seed=0)
