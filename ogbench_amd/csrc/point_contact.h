@@ -39,6 +39,7 @@
 
 #include "point_physics.h"
 
+
 namespace ogbx {
 
 // Full-loop active-set iterations before the damped-Newton safety net.  The
@@ -379,7 +380,10 @@ __device__ __forceinline__ void contact_loop(const PointModel& pm, const uint16_
   PieceWeights pw;
   piece_weights(act, pw);
   const int nstage = 4 * pm.nsub;
-#pragma unroll 20
+  // (by 4, not 20, for the rare full loop: the RK coefficients stay constants
+  // and the kernel's code shrinks by 1.3 MB; 11.55 -> 11.48 us per launch at
+  // N = 65,536, three A/B rounds.  The lean loop by 4: 12.45 us)
+#pragma unroll 4
   for (int e = 0; e < nstage; ++e) {
     const int st = e & 3;
     if (e != 0) {
