@@ -890,11 +890,11 @@ __global__ void __launch_bounds__(pwf_nt<WS>()) __attribute__((amdgpu_waves_per_
 // synchronized goal-replay step) the length of its task's goal sequence.
 // The order within a bucket is whatever the LDS atomics give: only the
 // schedule depends on it.
-__global__ void __launch_bounds__(1024) pwf_order_kernel(const PowderParams* __restrict__ Pp,
-                                                         const int32_t* __restrict__ ctrl,
-                                                         const uint32_t* __restrict__ cost, int32_t n,
-                                                         int32_t by_task, int32_t* __restrict__ order) {
-  __shared__ uint32_t hist[32];
+// One workgroup of NT threads (hist: 32 words of LDS).
+template <int NT>
+__device__ __forceinline__ void pwf_order_sort(const PowderParams* __restrict__ Pp, const int32_t* __restrict__ ctrl,
+                                               const uint32_t* __restrict__ cost, int32_t n, int32_t by_task,
+                                               int32_t* __restrict__ order, uint32_t* hist) {
   const int t = threadIdx.x;
   auto key = [&](int e) -> uint32_t {
     uint32_t c;
@@ -908,7 +908,7 @@ __global__ void __launch_bounds__(1024) pwf_order_kernel(const PowderParams* __r
   };
   if (t < 32) hist[t] = 0;
   __syncthreads();
-  for (int e = t; e < n; e += 1024) atomicAdd(&hist[key(e)], 1u);
+  for (int e = t; e < n; e += NT) atomicAdd(&hist[key(e)], 1u);
   __syncthreads();
   if (t == 0) {
     uint32_t run = 0;
@@ -919,7 +919,15 @@ __global__ void __launch_bounds__(1024) pwf_order_kernel(const PowderParams* __r
     }
   }
   __syncthreads();
-  for (int e = t; e < n; e += 1024) order[atomicAdd(&hist[key(e)], 1u)] = e;
+  for (int e = t; e < n; e += NT) order[atomicAdd(&hist[key(e)], 1u)] = e;
+}
+
+__global__ void __launch_bounds__(1024) pwf_order_kernel(const PowderParams* __restrict__ Pp,
+                                                         const int32_t* __restrict__ ctrl,
+                                                         const uint32_t* __restrict__ cost, int32_t n,
+                                                         int32_t by_task, int32_t* __restrict__ order) {
+  __shared__ uint32_t hist[32];
+  pwf_order_sort<1024>(Pp, ctrl, cost, n, by_task, order, hist);
 }
 
 // Render-only steps of medium/hard worlds (one step per launch).  An env at
@@ -940,12 +948,24 @@ __global__ void __launch_bounds__(256) pwf_light_step_kernel(
     const PowderParams* __restrict__ Pp, PowderState S, const int32_t* __restrict__ action,
     const int32_t* __restrict__ draws, uint8_t* __restrict__ obs, float* __restrict__ reward,
     uint8_t* __restrict__ terminated, uint8_t* __restrict__ truncated, uint8_t* __restrict__ success,
-    int32_t auto_reset, uint32_t a0, uint32_t a1, uint8_t* __restrict__ handled, int32_t refresh) {
+    int32_t auto_reset, uint32_t a0, uint32_t a1, uint8_t* __restrict__ handled, int32_t refresh,
+    int32_t order_mode, int32_t n, const uint32_t* __restrict__ cost, int32_t* __restrict__ order) {
   constexpr int C = WS * WS, CPT = C / 256;
   static_assert(CPT == 16 || CPT == 4, "64x64 or 32x32 worlds");
   __shared__ alignas(16) uint16_t st[C * 3];  // 6 observation bytes per cell
   __shared__ uint32_t lut[32];
-  const int64_t e = blockIdx.x;
+  // order_mode != 0 (the host expects the next step to be an in-phase full
+  // step): workgroup 0, dispatched first, sorts the envs for it as
+  // pwf_order_kernel would (1: by last cost, 2: by task length) beside this
+  // launch's render-only work instead of in a launch of its own before the
+  // full one.  It reads cost (written only by full steps) and ctrl's task bits
+  // (which no render-only step changes), so the order is the one the full
+  // step's own sort would give; env e is then workgroup e + 1.
+  if (order_mode != 0 && blockIdx.x == 0) {
+    pwf_order_sort<256>(Pp, S.ctrl, cost, n, order_mode == 2 ? 1 : 0, order, reinterpret_cast<uint32_t*>(st));
+    return;
+  }
+  const int64_t e = (int64_t)blockIdx.x - (order_mode != 0 ? 1 : 0);
   const uint64_t ge = (uint64_t)e + (uint64_t)Pp->env_base;  // global env index (Philox counter)
   const int t = threadIdx.x;
   if (t < 32) lut[t] = Pp->lut[t];
@@ -1280,6 +1300,11 @@ struct ogbx_powder_env {
   uint8_t* handled = nullptr;  // medium/hard: [N] env stepped by pwf_light_step_kernel this launch
   uint32_t* cost = nullptr;    // medium/hard: [N] shader cycles of the env's last one-env full-kernel workgroup
   int32_t* order = nullptr;    // medium/hard: [N] workgroup -> env of an in-phase full step, costliest first
+  // the last light launch sorted `order` for the step after it (by task
+  // length if order_by_task); consumed by that step when it is the in-phase
+  // full step the host expected.  A stale order is still a permutation of the
+  // envs: only the schedule would differ.
+  bool order_ready = false, order_by_task = false;
   bool light = true;           // split render-only steps into pwf_light_step_kernel
   // the render cache (S.crg / S.cb) may disagree with the state: set at create
   // and whenever a world or velocity pointer is handed out (the caller may
@@ -1548,6 +1573,7 @@ ogbx_status ogbx_powder_reset(ogbx_powder_t e, const int32_t* task_id, const uin
   OGBX_HIP(hipSetDevice(e->device));
   e->seed = seed;
   prep_invalidate(e);
+  e->order_ready = false;
   uint32_t k0, k1, r0, r1;
   seed_key(seed, kTagPowderReset, &k0, &k1);
   seed_key(seed, kTagPowderRand, &r0, &r1);
@@ -1613,10 +1639,24 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
       OGBX_HIP(hipEventRecord(e->ev_fork, (hipStream_t)stream));
       OGBX_HIP(hipStreamWaitEvent(e->side, e->ev_fork, 0));
     }
+    // the order of the next step's full launch, if the next step is an
+    // in-phase full step: sorted by a workgroup of this light launch
+    const bool had_order = e->order_ready;
+    const bool had_by_task = e->order_by_task;
+    e->order_ready = false;
+    int32_t order_mode = 0;
+    if (light && e->phase >= 0 && e->n <= INT32_MAX) {
+      const int64_t jn = (auto_reset && T > 0) ? (e->phase + 1) % T : e->phase + 1;
+      const bool sync_next = auto_reset && T > 0 && jn + 1 >= T;
+      if (jn % 3 == 2 || sync_next) order_mode = sync_next ? 2 : 1;
+    }
     if (light) {
-      PW_LAUNCH(pwf_light_step_kernel, e, (uint32_t)e->n, stream, e->Pd, e->S, action, draws, obs, reward,
-                terminated, truncated, success, auto_reset, a0, a1, e->handled, (int32_t)e->cache_stale);
+      PW_LAUNCH(pwf_light_step_kernel, e, (uint32_t)e->n + (order_mode ? 1u : 0u), stream, e->Pd, e->S, action, draws,
+                obs, reward, terminated, truncated, success, auto_reset, a0, a1, e->handled, (int32_t)e->cache_stale,
+                order_mode, (int32_t)e->n, e->cost, e->order);
       OGBX_LAUNCHED("pwf_light_step_kernel");
+      e->order_ready = order_mode != 0;
+      e->order_by_task = order_mode == 2;
     }
     // in phase, a render-only step leaves (nearly) no env to the full kernel
     if (light && e->phase >= 0) {
@@ -1635,9 +1675,11 @@ ogbx_status ogbx_powder_step(ogbx_powder_t e, const int32_t* action, int32_t k_s
         // a synchronized reset step replays by task length, unless it loads
         // prepared states (then the forward-cost order)
         const int32_t by_task = (auto_reset && T > 0 && j + 1 >= T && !prep.use) ? 1 : 0;
-        hipLaunchKernelGGL(pwf_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->Pd, e->S.ctrl, e->cost,
-                           (int32_t)e->n, by_task, e->order);
-        OGBX_LAUNCHED("pwf_order_kernel");
+        if (!(had_order && had_by_task == (by_task != 0))) {
+          hipLaunchKernelGGL(pwf_order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, e->Pd, e->S.ctrl, e->cost,
+                             (int32_t)e->n, by_task, e->order);
+          OGBX_LAUNCHED("pwf_order_kernel");
+        }
         order = e->order;
       }
       PWF_LAUNCH(pwf_step_kernel_dense, e, (uint32_t)e->n, stream, e->Pd, e->S, e->n, action, draws, rand, k_steps,
